@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident aggregate+unmask GB/s for Flamingo's server round.
+
+Contract (see README/DESIGN.md): ``python bench.py --gpus N --steps K --warmup W``
+prints ONE JSON line on rank 0.  For N > 1 it is launched by torch.distributed.run
+(one process per GPU, RCCL over xGMI).
+
+Workload (BASELINE.json configs[3], "c4"): every GPU ingests 1024 clients'
+masked vectors of L = 2^20 uint32 slots; the round has N_total = 1024 * G
+clients, no dropouts, so K = N_total self-mask seeds are regenerated
+(SA_ServiceAgent.py:529-536) and the output is sum(y_i) - sum PRG(m_i) = |U|
+in every slot (checked after timing).  Per-GPU work is fixed as G grows
+(weak scaling): rows 1024 x L per GPU, masks K x L/G per GPU.
+
+A step = one round on device-resident inputs: seed-schedule launch +
+row-sum/unmask launch (+ RCCL reduce-scatter of the L-slot partial for G > 1).
+value = algorithmic bytes (4*|U|*L read + 4*L written) / max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident aggregate+unmask GB/s, N clients × L int32 per round"
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 Tops/s
+CHACHA_OPS_PER_WORD = 60.4       # VALU instructions per mask word in items_kernel (.s count)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clients-per-gpu", type=int, default=1024)
+    ap.add_argument("--log2-L", type=int, default=20)
+    ap.add_argument("--dropout", type=float, default=0.0, help="fraction of clients offline (c5: 0.01)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-copy", action="store_true", help="skip the PCIe-inclusive measurement")
+    ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")
+    ap.add_argument("--profile", action="store_true", help="minimal run for rocprofv3 (no CPU/copy legs)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    if args.gpus != world and not (world == 1 and args.gpus == 1):
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    G = world
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from flamingo_amd import MaskEngine
+    from flamingo_amd import params as P
+    from flamingo_amd.distributed import ShardedRound, client_bounds
+
+    eng = MaskEngine(torch.cuda.current_device())
+    L = 1 << args.log2_L
+    Ng = args.clients_per_gpu
+    N = Ng * G
+    cfg = f"c4-n{N}-L{L}"
+
+    # ---- inputs: valid masked rows, built on this GPU by the client-side kernel
+    m = np.frombuffer(b"".join(P.bench_seed(cfg, i) for i in range(N)), np.uint8).reshape(N, 32)
+    nbrs = P.neighbor_graph(b"\x00" * 32, 1, N, 1, encrypt=eng.chacha20_encrypt)
+    c0, c1 = client_bounds(N, G, rank)
+    # client seed table of my clients (ids are global: SA_ClientAgent.py:304-324)
+    seg_l, seeds_l, signs_l = [0], [], []
+    for i in range(c0, c1):
+        seeds_l.append(m[i].tobytes()); signs_l.append(1)
+        for j in sorted(nbrs[i]):
+            seeds_l.append(P.synthetic_pair_seed(i, j)); signs_l.append(1 if i < j else -1)
+        seg_l.append(len(seeds_l))
+    seg = np.array(seg_l, np.int64)
+    cseeds = np.frombuffer(b"".join(seeds_l), np.uint8).reshape(-1, 32)
+    csigns = np.array(signs_l, np.int8)
+    rows = torch.empty((c1 - c0, L), dtype=torch.int32, device=dev)
+    eng.client_mask_dev(seg, torch.from_numpy(cseeds.copy()).to(dev), csigns, rows, L)
+
+    g = np.random.Generator(np.random.PCG64(12345))
+    n_off = int(round(args.dropout * N))
+    offline = np.sort(g.choice(N, n_off, replace=False)) if n_off else np.zeros(0, np.int64)
+    online = np.setdiff1d(np.arange(N), offline)
+    sseeds, ssigns = P.server_seed_table(m, nbrs, online, offline, P.synthetic_pair_seed)
+    K = sseeds.shape[0]
+    D = K - len(online)
+    my_online = online[(online >= c0) & (online < c1)] - c0
+    rows_on = rows if len(my_online) == rows.shape[0] else rows[torch.from_numpy(my_online).to(dev)].contiguous()
+    d_seeds = torch.from_numpy(sseeds).to(dev)
+    d_signs = torch.from_numpy(ssigns).to(dev)
+    torch.cuda.synchronize()
+
+    rnd = ShardedRound(eng, L)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        rnd.prepare_seeds(d_seeds, d_signs, stream)
+        ev_k[0].record(stream)
+        rnd.compute(rows_on, stream)
+        ev_k[1].record(stream)
+        return rnd.exchange()
+
+    ev_k = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if G > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        # per-launch kernel time read back without stalling the next launch
+        kern_ms.append((ev_k[0], ev_k[1]))
+        ev_k = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    torch.cuda.synchronize()
+    if G > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if G > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kms = float(np.mean([a.elapsed_time(b) for a, b in kern_ms]))
+
+    # ---- correctness of the timed round: out == |U| in every slot of my shard
+    out = rnd.exchange() if G > 1 else rnd.partial[:L]
+    torch.cuda.synchronize()
+    ok = bool(torch.all(out == len(online)).item())
+    okt = torch.tensor([1 if ok else 0], device=dev)
+    if G > 1:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    ok = bool(okt.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    bytes_round = 4.0 * len(online) * L + 4.0 * L
+    value = bytes_round / (elapsed / args.steps) / 1e9
+    rows_rank = rows_on.shape[0]
+    mask_slots = rnd.hi - rnd.lo
+    ach_gbs = (4.0 * rows_rank * L + 4.0 * L) / (kms * 1e-3) / 1e9
+    words = float(K) * mask_slots
+    valu_tops = words * CHACHA_OPS_PER_WORD / (kms * 1e-3) / 1e12
+
+    res = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "correct": ok,
+        "data": "synthetic: valid masked rows y_i = 1 + PRG(m_i) +- PRG(s_ij) made on-GPU from SHA-256 bench "
+                "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
+        "config": {"workload": "c4: aggregate + self-mask and dropout-pair unmask, one server round",
+                   "clients": N, "clients_per_gpu": Ng, "online": int(len(online)), "L": L, "seeds_K": int(K),
+                   "dropout_pairs_D": int(D), "global_batch": N, "seq_len": L,
+                   "parallelism": f"client-shard{G}+slot-shard{G}" + ("+rccl-reduce-scatter" if G > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "items_kernel<1>", "kernel_ms": round(kms, 4),
+                     "bytes_per_launch": 4 * rows_rank * L + 4 * L},
+        "roofline_valu": {"bound": "valu", "mask_words_per_launch": int(words), "ops_per_word": CHACHA_OPS_PER_WORD,
+                          "achieved_tops": round(valu_tops, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
+                          "frac": round(valu_tops / VALU_PEAK_TOPS, 4)},
+    }
+
+    if rank == 0 and G == 1 and not args.profile:
+        if not args.no_variants:
+            res["variants"] = variant_pairs_only(eng, torch, rows_on, m, nbrs, online, L, stream, P)
+        if not args.no_copy:
+            res["with_copy"] = with_copy(eng, torch, rows_on, sseeds, ssigns, L, len(online))
+        if not args.no_cpu:
+            res["cpu_baseline"] = cpu_baseline(rows_on, sseeds, ssigns, L, out)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if G > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return 0 if ok else 1
+
+
+def variant_pairs_only(eng, torch, rows, m, nbrs, online, L, stream, P):
+    """Aggregate + dropout-pair unmask only (K = D), the HBM-bound half of the round."""
+    N = rows.shape[0]
+    g = np.random.Generator(np.random.PCG64(99))
+    off = np.sort(g.choice(N, max(1, N // 100), replace=False))
+    on = np.setdiff1d(np.arange(N), off)
+    pairs, pairs_signs = P.dropout_pairs(nbrs, on, off)
+    seeds = np.frombuffer(b"".join(P.synthetic_pair_seed(i, j) for i, j in pairs), np.uint8).reshape(-1, 32)
+    d_seeds = torch.from_numpy(seeds.copy()).cuda()
+    d_signs = torch.from_numpy(np.array(pairs_signs, np.int8)).cuda()
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    K = seeds.shape[0]
+    res = {}
+    for name, rr in (("pairs_only", rows),):
+        eng.seed_table_dev(d_seeds, d_signs, stream=stream)
+        for _ in range(3):
+            eng.aggregate_dev(rr, K, out, L=L, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        reps = 20
+        for _ in range(reps):
+            eng.aggregate_dev(rr, K, out, L=L, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = (4.0 * rr.shape[0] * L + 4.0 * L) / (ms * 1e-3) / 1e9
+        res[name] = {"rows": int(rr.shape[0]), "seeds_K": int(K), "kernel_ms": round(ms, 4), "GB/s": round(gbs, 1),
+                     "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "note": "rows summed + dropout-pair masks only (self masks excluded): HBM-bound half"}
+    return res
+
+
+def with_copy(eng, torch, rows, seeds, signs, L, n_online):
+    """PCIe-inclusive round: pinned host rows -> device -> round -> host out."""
+    from flamingo_amd import PinnedArena
+    N = rows.shape[0]
+    arena = PinnedArena(N * L * 4 + L * 4 + 4096)
+    host = arena.array((N, L), np.uint32)
+    host_out = arena.array((L,), np.uint32)
+    host.view(np.int32)[:] = rows.cpu().numpy()
+    vecs = [host[i] for i in range(N)]
+    t = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = eng.aggregate_unmask(vecs, seeds, signs, L=L)
+        t.append(time.perf_counter() - t0)
+    ok = bool(np.all(out == n_online))
+    arena.free()
+    best = min(t)
+    return {"ms_per_round": round(best * 1e3, 2), "GB/s": round((4.0 * N * L + 4.0 * L) / best / 1e9, 2),
+            "correct": ok, "path": "flm_aggregate_unmask: per-row hipMemcpyAsync from pinned host + D2H of out"}
+
+
+def cpu_baseline(rows, seeds, signs, L, gpu_out):
+    """The C restatement (oracle/, scalar, 1 thread) on this host, same inputs; also cross-checks the GPU."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # checker / CPU baseline only
+    N = rows.shape[0]
+    host = rows.cpu().numpy().view(np.uint32)
+    res = {}
+    t0 = time.perf_counter()
+    out = O.aggregate_unmask(host, seeds, signs, L=L, threads=1)
+    dt = time.perf_counter() - t0
+    same = bool(np.array_equal(out, gpu_out.cpu().numpy().view(np.uint32)))
+    res.update({"value": round((4.0 * N * L + 4.0 * L) / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+                "sample": f"the full workload: {N} rows x {L} slots, {seeds.shape[0]} seeds, 1 thread",
+                "seconds": round(dt, 3), "matches_gpu": same,
+                "cpu": platform.processor() or platform.machine()})
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    out2 = O.aggregate_unmask(host, seeds, signs, L=L, threads=threads)
+    dt2 = time.perf_counter() - t0
+    res["all_cores"] = {"value": round((4.0 * N * L + 4.0 * L) / dt2 / 1e9, 3), "cores": threads,
+                        "seconds": round(dt2, 3), "matches_gpu": bool(np.array_equal(out2, out))}
+    return res
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,41 @@
+"""Build libflamingo_hip.so in-tree for gfx950 (hipcc, no JIT cache).
+
+``python -m flamingo_amd.build`` or ``flamingo_amd.build.build()``.  The .so
+lands in flamingo_amd/lib/ (git-ignored, shipped to the GPU box with the tree).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = [os.path.join(HERE, "csrc", f) for f in ("flm_kernels.hip", "flm_runtime.hip")]
+HDRS = [os.path.join(HERE, "csrc", "flm_internal.h"),
+        os.path.join(os.path.dirname(HERE), "include", "flamingo_hip.h")]
+OUT = os.path.join(HERE, "lib", "libflamingo_hip.so")
+ARCH = os.environ.get("FLM_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in SRC + HDRS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-o", OUT + ".tmp"] + SRC
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

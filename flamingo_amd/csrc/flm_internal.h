@@ -1,0 +1,76 @@
+// flm_internal.h -- shared between the gfx950 kernels (flm_kernels.hip) and the
+// host runtime (flm_runtime.hip).  Not part of the public ABI.
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include <hip/hip_runtime.h>
+
+namespace flm {
+
+// b"abcd" as a little-endian word (util/param.py:12).
+constexpr uint32_t kAbcd = 0x64636261u;
+// ChaCha20 "expand 32-byte k".
+constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
+                   kSigma3 = 0x6b206574u;
+
+// One wave owns a 1024-slot sub-tile: 64 lanes x one 16-word ChaCha block.
+constexpr int kWaveSlots = 1024;
+constexpr int kWavesPerGroup = 16;          // 1024-thread workgroups
+constexpr int kThreads = 64 * kWavesPerGroup;
+
+// Per-seed schedule, built on the device by seed_schedule_kernel: the key, the
+// sign folded into an XOR constant, and everything of ChaCha's first double
+// round that does not depend on the block counter (block counter high word is
+// 0 for every slot < 2^36, nonce is zero).  128 bytes, read with scalar loads.
+struct SeedRec {
+    uint32_t k[8];     // key words (LE32 of the 32 seed bytes)
+    uint32_t xorc;     // 0x64636261 for sign +1, ~0x64636261 for sign -1
+    uint32_t a0;       // sigma0 + k0 (first add of column 0)
+    uint32_t col1[4];  // x1, x5, x9, x13 after round-1 column QR(1,5,9,13)
+    uint32_t col2[4];  // x2, x6, x10, x14 after QR(2,6,10,14)
+    uint32_t col3[4];  // x3, x7, x11, x15 after QR(3,7,11,15)
+    uint32_t d1a;      // x1 + x6   (first step of diagonal QR(1,6,11,12))
+    uint32_t d2a;      // x2 + x7   (first step of diagonal QR(2,7,8,13))
+    uint32_t d2d;      // rotl(x13 ^ d2a, 16)
+    uint32_t pad[7];
+};
+static_assert(sizeof(SeedRec) == 128, "SeedRec must be 128 bytes");
+
+enum ItemFlags : uint32_t {
+    kHasRows = 1u,
+    kHasMask = 2u,
+    kSameTile = 4u,       // row tile == mask tile: combine before writing
+    kRowAtomic = 8u,      // row (or combined) tile written with u32 atomic adds
+    kMaskAtomic = 16u,
+    kMaskBiasNneg = 32u,  // add the device-side count of negative signs to the mask tile
+};
+
+// One workgroup's work: a row unit (sum of `nrows` rows over one tile) and/or a
+// mask unit (sum of seeds [k0, k0+nseeds) over one tile).  64 bytes.
+struct Item {
+    uint64_t row_in;     // element offset into rows: first row of the unit, tile start slot
+    uint64_t row_out;    // element offset into out of the row tile
+    uint64_t mask_out;   // element offset into out of the mask tile
+    uint64_t mask_ctr;   // ChaCha block counter at the mask tile start (PRG slot / 16)
+    uint32_t nrows;
+    uint32_t k0;
+    uint32_t nseeds;
+    uint32_t row_valid;  // valid slots in the row tile (tail)
+    uint32_t mask_valid;
+    uint32_t flags;
+    uint32_t row_bias;   // added once per slot of the row tile
+    uint32_t mask_bias;  // added once per slot of the mask tile
+};
+static_assert(sizeof(Item) == 64, "Item must be 64 bytes");
+
+// Launchers (flm_kernels.hip).  All enqueue on `stream` and return hipError_t.
+hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
+                                uint32_t *d_meta, hipStream_t stream);
+// subtiles: 1, 4 or 16 sub-tiles of 1024 slots per workgroup.
+hipError_t launch_items(int subtiles, const Item *d_items, int n_items, const uint32_t *d_rows,
+                        uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta,
+                        uint32_t *d_out, hipStream_t stream);
+hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
+                               const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
+
+}  // namespace flm

@@ -1,0 +1,400 @@
+// flm_kernels.hip -- gfx950 (CDNA4) kernels for Flamingo's mask-and-aggregate path.
+//
+// Reference behaviour (paths relative to the reference root):
+//   PRG(seed)[l] = LE32(ChaCha20_DJB(seed, nonce 0^8) word l) ^ 0x64636261
+//     -- ChaCha20.new(key=seed, nonce=param.nonce).encrypt(param.fixed_key*L)
+//        + np.frombuffer(..,'uint32'): agent/flamingo/SA_ServiceAgent.py:533-536,
+//        596-603; agent/flamingo/SA_ClientAgent.py:248-250, 296-298.
+//   partial sum        S = sum_i y_i          SA_ServiceAgent.py:346-350
+//   self-mask unmask   M = -sum_i PRG(m_i)    SA_ServiceAgent.py:529-536
+//   dropout-pair unmask C = sum sigma PRG(s)  SA_ServiceAgent.py:587-603
+//   final              out = S + C + M        SA_ServiceAgent.py:538-540, 605
+//   client masking     y = x + PRG(m) +- PRG(s_ij)   SA_ClientAgent.py:304-324
+//
+// Design (MI355X-first):
+//   * Integer elementwise work: VALU only, no MFMA.  ChaCha20 is ~59 VALU ops
+//     per output word, so regenerating masks is VALU-bound; summing rows is
+//     HBM-bound.  One kernel does both so the two overlap inside every wave.
+//   * A wave owns a 1024-slot sub-tile.  Masks are generated in "block layout"
+//     (lane t computes ChaCha block t: slots 16t..16t+15) and never written to
+//     HBM; rows are streamed in "coalesced layout" (lane t loads 16 B at
+//     slot 4t + 256j, j = 0..3: every load instruction is 1 KiB contiguous).
+//     The two layouts meet once per work item, through LDS.
+//   * Signs fold into the XOR constant: -(ks ^ C) = (ks ^ ~C) + 1 mod 2^32, so
+//     every seed costs one v_xad_u32 per word and the "+1" per negative seed
+//     is added once per slot as a bias (count kept on the device).
+//   * Everything of ChaCha's first double round that does not depend on the
+//     block counter is computed once per seed (SeedRec), not per block.
+//   * 1024-thread workgroups: 16 waves split an item's rows/seeds, partial
+//     sums are combined through LDS; tiles shared by several items are
+//     combined with u32 atomics (exact: integer adds commute).
+#include "flm_internal.h"
+
+namespace flm {
+
+#define FLM_ROTL(v, c) __builtin_rotateleft32((v), (c))
+#define FLM_QR(a, b, c, d)                       \
+    a += b; d ^= a; d = FLM_ROTL(d, 16);          \
+    c += d; b ^= c; b = FLM_ROTL(b, 12);          \
+    a += b; d ^= a; d = FLM_ROTL(d, 8);           \
+    c += d; b ^= c; b = FLM_ROTL(b, 7);
+
+// ------------------------------------------------------------------ seeds
+// Host-side twin of the first column round lives nowhere else: the schedule
+// is computed on the device from the raw seed bytes.
+__global__ __launch_bounds__(1024) void seed_schedule_kernel(const uint8_t *__restrict__ seeds,
+                                                             const int8_t *__restrict__ signs, int K,
+                                                             SeedRec *__restrict__ recs,
+                                                             uint32_t *__restrict__ meta) {
+    __shared__ uint32_t s_neg, s_bad;
+    if (threadIdx.x == 0) { s_neg = 0; s_bad = 0; }
+    __syncthreads();
+    uint32_t neg = 0, bad = 0;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+        const uint8_t *p = seeds + 32 * (size_t)k;
+        uint32_t key[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            key[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
+                     ((uint32_t)p[4 * i + 3] << 24);
+        const int s = signs[k];
+        neg += (s < 0);
+        bad += (s != 1 && s != -1);
+        SeedRec r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.k[i] = key[i];
+        r.xorc = s < 0 ? ~kAbcd : kAbcd;
+        r.a0 = kSigma0 + key[0];
+        uint32_t x1 = kSigma1, x5 = key[1], x9 = key[5], x13 = 0u;
+        uint32_t x2 = kSigma2, x6 = key[2], x10 = key[6], x14 = 0u;
+        uint32_t x3 = kSigma3, x7 = key[3], x11 = key[7], x15 = 0u;
+        FLM_QR(x1, x5, x9, x13);
+        FLM_QR(x2, x6, x10, x14);
+        FLM_QR(x3, x7, x11, x15);
+        r.col1[0] = x1; r.col1[1] = x5; r.col1[2] = x9; r.col1[3] = x13;
+        r.col2[0] = x2; r.col2[1] = x6; r.col2[2] = x10; r.col2[3] = x14;
+        r.col3[0] = x3; r.col3[1] = x7; r.col3[2] = x11; r.col3[3] = x15;
+        r.d1a = x1 + x6;
+        r.d2a = x2 + x7;
+        r.d2d = FLM_ROTL(x13 ^ r.d2a, 16);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) r.pad[i] = 0;
+        recs[k] = r;
+    }
+    if (neg) atomicAdd(&s_neg, neg);
+    if (bad) atomicAdd(&s_bad, bad);
+    __syncthreads();
+    if (threadIdx.x == 0) { meta[0] = s_neg; meta[1] = s_bad; }
+}
+
+// -------------------------------------------------------------- ChaCha core
+// m[i] += ChaCha20_block(seed, ctr)[i] ^ xorc for the 16 words of block `ctr`.
+// `rec` is wave-uniform (scalar loads); `ctr` is per lane.
+__device__ __forceinline__ void chacha_mask_add(const SeedRec *__restrict__ rec, uint32_t ctr,
+                                                uint32_t (&m)[16]) {
+    const uint32_t k0 = rec->k[0], k1 = rec->k[1], k2 = rec->k[2], k3 = rec->k[3];
+    const uint32_t k4 = rec->k[4], k5 = rec->k[5], k6 = rec->k[6], k7 = rec->k[7];
+    const uint32_t xc = rec->xorc;
+    uint32_t x0, x1, x2, x3, x4, x5, x6, x7, x8, x9, x10, x11, x12, x13, x14, x15;
+    // round 1, column QR(0,4,8,12): a = sigma0 + k0 precomputed
+    x0 = rec->a0;
+    x12 = FLM_ROTL(ctr ^ x0, 16);
+    x8 = k4 + x12;
+    x4 = FLM_ROTL(k0 ^ x8, 12);
+    x0 += x4;
+    x12 = FLM_ROTL(x12 ^ x0, 8);
+    x8 += x12;
+    x4 = FLM_ROTL(x4 ^ x8, 7);
+    // round 1, columns 1..3: counter independent
+    x1 = rec->col1[0]; x5 = rec->col1[1]; x9 = rec->col1[2]; x13 = rec->col1[3];
+    x2 = rec->col2[0]; x6 = rec->col2[1]; x10 = rec->col2[2]; x14 = rec->col2[3];
+    x3 = rec->col3[0]; x7 = rec->col3[1]; x11 = rec->col3[2]; x15 = rec->col3[3];
+    // round 1, diagonals
+    FLM_QR(x0, x5, x10, x15);
+    x1 = rec->d1a;  // QR(1,6,11,12) from its second step
+    x12 ^= x1; x12 = FLM_ROTL(x12, 16);
+    x11 += x12; x6 ^= x11; x6 = FLM_ROTL(x6, 12);
+    x1 += x6; x12 ^= x1; x12 = FLM_ROTL(x12, 8);
+    x11 += x12; x6 ^= x11; x6 = FLM_ROTL(x6, 7);
+    x2 = rec->d2a;  // QR(2,7,8,13) from its fourth step
+    x13 = rec->d2d;
+    x8 += x13; x7 ^= x8; x7 = FLM_ROTL(x7, 12);
+    x2 += x7; x13 ^= x2; x13 = FLM_ROTL(x13, 8);
+    x8 += x13; x7 ^= x8; x7 = FLM_ROTL(x7, 7);
+    FLM_QR(x3, x4, x9, x14);
+    // rounds 2..10
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        FLM_QR(x0, x4, x8, x12);
+        FLM_QR(x1, x5, x9, x13);
+        FLM_QR(x2, x6, x10, x14);
+        FLM_QR(x3, x7, x11, x15);
+        FLM_QR(x0, x5, x10, x15);
+        FLM_QR(x1, x6, x11, x12);
+        FLM_QR(x2, x7, x8, x13);
+        FLM_QR(x3, x4, x9, x14);
+    }
+    // feed-forward (input words 13..15 are zero), fold "abcd"/sign, accumulate
+    m[0] += (x0 + kSigma0) ^ xc;
+    m[1] += (x1 + kSigma1) ^ xc;
+    m[2] += (x2 + kSigma2) ^ xc;
+    m[3] += (x3 + kSigma3) ^ xc;
+    m[4] += (x4 + k0) ^ xc;
+    m[5] += (x5 + k1) ^ xc;
+    m[6] += (x6 + k2) ^ xc;
+    m[7] += (x7 + k3) ^ xc;
+    m[8] += (x8 + k4) ^ xc;
+    m[9] += (x9 + k5) ^ xc;
+    m[10] += (x10 + k6) ^ xc;
+    m[11] += (x11 + k7) ^ xc;
+    m[12] += (x12 + ctr) ^ xc;
+    m[13] += x13 ^ xc;
+    m[14] += x14 ^ xc;
+    m[15] += x15 ^ xc;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Load the wave's 4 KiB of one row in coalesced layout through a buffer
+// descriptor whose range ends at the tile's last valid quad: quads past it
+// (tail tile) come back as zero from the hardware range check, no branches.
+__device__ __forceinline__ void load_row(const uint32_t *base, uint32_t bytes, int lane, u32x4 (&v)[4]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(base), 0,
+                                                                        (int)bytes, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane + 1024 * j, 0, 0));
+}
+
+// Sum the Cw chunk partials of every sub-tile from LDS and write the tile.
+template <int S>
+__device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32_t *__restrict__ out,
+                                           uint64_t base, int valid, uint32_t bias, bool atomic) {
+    constexpr int Cw = kWavesPerGroup / S;
+    if (!atomic) {
+        for (int q = threadIdx.x; q < S * 256; q += kThreads) {
+            const int s = q >> 8, p = q & 255;
+            u32x4 acc = u32x4(bias);
+#pragma unroll
+            for (int c = 0; c < Cw; ++c) acc = acc + lds[(s + S * c) * 256 + p];
+            const int slot = s * kWaveSlots + 4 * p;
+            uint32_t *dst = out + base + slot;
+            if (slot + 3 < valid) {
+                *reinterpret_cast<u32x4 *>(dst) = acc;
+            } else {
+                if (slot + 0 < valid) dst[0] = acc.x;
+                if (slot + 1 < valid) dst[1] = acc.y;
+                if (slot + 2 < valid) dst[2] = acc.z;
+            }
+        }
+    } else {
+        const uint32_t *l32 = reinterpret_cast<const uint32_t *>(lds);
+        for (int d = threadIdx.x; d < S * kWaveSlots; d += kThreads) {
+            const int s = d >> 10, o = d & 1023;
+            uint32_t acc = bias;
+#pragma unroll
+            for (int c = 0; c < Cw; ++c) acc += l32[(s + S * c) * 1024 + o];
+            const int slot = s * kWaveSlots + o;
+            if (slot < valid) atomicAdd(out + base + slot, acc);
+        }
+    }
+}
+
+// --------------------------------------------------------------- main kernel
+// One workgroup = one Item.  Wave w works on sub-tile s = w % S with chunk
+// c = w / S of the item's rows and seeds (Cw = 16 / S chunks).
+template <int S>
+__global__ __launch_bounds__(kThreads) void items_kernel(const Item *__restrict__ items,
+                                                         const uint32_t *__restrict__ rows,
+                                                         uint64_t row_pitch,
+                                                         const SeedRec *__restrict__ recs,
+                                                         const uint32_t *__restrict__ meta,
+                                                         uint32_t *__restrict__ out) {
+    constexpr int Cw = kWavesPerGroup / S;
+    __shared__ u32x4 lds[kWavesPerGroup * 256];  // 64 KiB: one 4 KiB region per wave
+
+    const Item it = items[blockIdx.x];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int s = w % S, c = w / S;
+    const uint32_t flags = it.flags;
+    const bool has_rows = flags & kHasRows, has_mask = flags & kHasMask;
+
+    u32x4 racc[4] = {u32x4(0u), u32x4(0u), u32x4(0u), u32x4(0u)};
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = 0;
+
+    // this wave's share of rows and seeds
+    uint32_t nr = 0, ns = 0, r0 = 0, q0 = 0;
+    if (has_rows) {
+        r0 = (uint32_t)(((uint64_t)it.nrows * c) / Cw);
+        nr = (uint32_t)(((uint64_t)it.nrows * (c + 1)) / Cw) - r0;
+    }
+    if (has_mask) {
+        q0 = it.k0 + (uint32_t)(((uint64_t)it.nseeds * c) / Cw);
+        ns = it.k0 + (uint32_t)(((uint64_t)it.nseeds * (c + 1)) / Cw) - q0;
+    }
+    const int sub_slot = s * kWaveSlots;
+    const int row_valid = (int)it.row_valid - sub_slot;   // may be <= 0: nothing valid
+    // bytes of this sub-tile a row load may touch: whole quads up to the last valid slot
+    const uint32_t row_bytes =
+        row_valid >= kWaveSlots ? 4u * kWaveSlots : (row_valid > 0 ? 16u * (uint32_t)((row_valid + 3) / 4) : 0u);
+    const uint32_t *rp = rows + it.row_in + (uint64_t)r0 * row_pitch + sub_slot;
+    const uint32_t ctr = (uint32_t)(it.mask_ctr + (uint64_t)(sub_slot / 16) + (uint64_t)lane);
+    const SeedRec *rec = recs + q0;
+
+    if (row_valid <= 0) nr = 0;
+    // paired phase: one row load in flight under one ChaCha block per step
+    const uint32_t np = nr < ns ? nr : ns;
+    for (uint32_t q = 0; q < np; ++q) {
+        u32x4 v[4];
+        load_row(rp, row_bytes, lane, v);
+        chacha_mask_add(rec, ctr, m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[j];
+        rp += row_pitch;
+        ++rec;
+    }
+    // remaining rows: four rows (16 KiB per wave) in flight
+    uint32_t rr = nr - np;
+    for (; rr >= 4; rr -= 4) {
+        u32x4 v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load_row(rp + u * row_pitch, row_bytes, lane, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[u][j];
+        rp += 4 * row_pitch;
+    }
+    for (; rr > 0; --rr) {
+        u32x4 v[4];
+        load_row(rp, row_bytes, lane, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[j];
+        rp += row_pitch;
+    }
+    // remaining seeds
+    for (uint32_t q = np; q < ns; ++q) {
+        chacha_mask_add(rec, ctr, m);
+        ++rec;
+    }
+
+    // ---- combine: block layout -> coalesced layout through this wave's LDS region
+    u32x4 *R = lds + w * 256;
+    const bool same = flags & kSameTile;
+    u32x4 mq[4];
+    if (has_mask) {
+        R[4 * lane + 0] = u32x4{m[0], m[1], m[2], m[3]};
+        R[4 * lane + 1] = u32x4{m[4], m[5], m[6], m[7]};
+        R[4 * lane + 2] = u32x4{m[8], m[9], m[10], m[11]};
+        R[4 * lane + 3] = u32x4{m[12], m[13], m[14], m[15]};
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mq[j] = R[lane + 64 * j];
+        if (same) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) racc[j] = racc[j] + mq[j];
+        }
+    }
+    const uint32_t nneg = meta[0];
+    const uint32_t mbias = it.mask_bias + ((flags & kMaskBiasNneg) ? nneg : 0u);
+    if (has_rows || same) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[lane + 64 * j] = racc[j];
+        __syncthreads();
+        const uint64_t base = same ? it.mask_out : it.row_out;
+        const int valid = same ? (int)it.mask_valid : (int)it.row_valid;
+        const uint32_t bias = it.row_bias + (same ? mbias : 0u);
+        const bool atom = same ? ((flags & (kRowAtomic | kMaskAtomic)) != 0) : ((flags & kRowAtomic) != 0);
+        reduce_out<S>(lds, out, base, valid, bias, atom);
+    }
+    if (has_mask && !same) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[lane + 64 * j] = mq[j];
+        __syncthreads();
+        reduce_out<S>(lds, out, it.mask_out, (int)it.mask_valid, mbias, (flags & kMaskAtomic) != 0);
+    }
+}
+
+// --------------------------------------------------- byte keystream (host PRF)
+// out = in ^ ChaCha20(key, nonce) from block `counter`, one block per thread.
+__global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t k1, uint32_t k2,
+                                                           uint32_t k3, uint32_t k4, uint32_t k5,
+                                                           uint32_t k6, uint32_t k7, uint32_t n0,
+                                                           uint32_t n1, uint64_t counter,
+                                                           const uint8_t *__restrict__ in,
+                                                           uint8_t *__restrict__ out, uint64_t n) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t off = b * 64;
+    if (off >= n) return;
+    const uint64_t blk = counter + b;
+    uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
+    uint32_t x4 = k0, x5 = k1, x6 = k2, x7 = k3, x8 = k4, x9 = k5, x10 = k6, x11 = k7;
+    uint32_t x12 = (uint32_t)blk, x13 = (uint32_t)(blk >> 32), x14 = n0, x15 = n1;
+    const uint32_t i12 = x12, i13 = x13;
+    for (int r = 0; r < 10; ++r) {
+        FLM_QR(x0, x4, x8, x12);
+        FLM_QR(x1, x5, x9, x13);
+        FLM_QR(x2, x6, x10, x14);
+        FLM_QR(x3, x7, x11, x15);
+        FLM_QR(x0, x5, x10, x15);
+        FLM_QR(x1, x6, x11, x12);
+        FLM_QR(x2, x7, x8, x13);
+        FLM_QR(x3, x4, x9, x14);
+    }
+    const uint32_t ks[16] = {x0 + kSigma0, x1 + kSigma1, x2 + kSigma2, x3 + kSigma3,
+                             x4 + k0,      x5 + k1,      x6 + k2,      x7 + k3,
+                             x8 + k4,      x9 + k5,      x10 + k6,     x11 + k7,
+                             x12 + i12,    x13 + i13,    x14 + n0,     x15 + n1};
+    const uint64_t m = (n - off) < 64 ? (n - off) : 64;
+    for (uint64_t i = 0; i < m; ++i) out[off + i] = in[off + i] ^ (uint8_t)(ks[i >> 2] >> (8 * (i & 3)));
+}
+
+#undef FLM_QR
+#undef FLM_ROTL
+
+// ----------------------------------------------------------------- launchers
+hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
+                                uint32_t *d_meta, hipStream_t stream) {
+    hipLaunchKernelGGL(seed_schedule_kernel, dim3(1), dim3(1024), 0, stream, d_seeds, d_signs, K, d_recs,
+                       d_meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_items(int subtiles, const Item *d_items, int n_items, const uint32_t *d_rows,
+                        uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta,
+                        uint32_t *d_out, hipStream_t stream) {
+    if (n_items <= 0) return hipSuccess;
+    switch (subtiles) {
+        case 1:
+            hipLaunchKernelGGL(items_kernel<1>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+                               row_pitch, d_recs, d_meta, d_out);
+            break;
+        case 4:
+            hipLaunchKernelGGL(items_kernel<4>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+                               row_pitch, d_recs, d_meta, d_out);
+            break;
+        case 16:
+            hipLaunchKernelGGL(items_kernel<16>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+                               row_pitch, d_recs, d_meta, d_out);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
+                               const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 63) / 64;
+    const unsigned grid = (unsigned)((blocks + 255) / 256);
+    hipLaunchKernelGGL(chacha20_xor_kernel, dim3(grid), dim3(256), 0, stream, key[0], key[1], key[2], key[3],
+                       key[4], key[5], key[6], key[7], nonce[0], nonce[1], counter, d_in, d_out, (uint64_t)n);
+    return hipGetLastError();
+}
+
+}  // namespace flm

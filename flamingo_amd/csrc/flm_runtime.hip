@@ -1,0 +1,655 @@
+// flm_runtime.hip -- host runtime and C ABI of libflamingo_hip.so (include/flamingo_hip.h).
+//
+// Owns one GPU per context: its stream, grow-on-demand device buffers, the
+// per-shape launch plans (work-item tables) and the error string.  The launch
+// planner turns a round's shape into Items (flm_internal.h) so that every
+// workgroup carries an equal share of row streaming and mask generation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/flamingo_hip.h"
+#include "flm_internal.h"
+
+using flm::Item;
+using flm::SeedRec;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+};
+
+// One contiguous job of the planner: out[out_base + l] for l in [0, L) gets the
+// sum of `nrows` rows (rows_base + r*pitch + l) and, for l in [mask_lo, mask_hi),
+// seeds [k0, k0+nseeds) at PRG slot prg_slot0 + l, plus mask_bias.
+struct Job {
+    uint64_t out_base = 0, rows_base = 0;
+    uint32_t nrows = 0;
+    uint64_t L = 0;
+    uint32_t k0 = 0, nseeds = 0;
+    uint64_t mask_lo = 0, mask_hi = 0, prg_slot0 = 0;
+    uint32_t mask_bias = 0;
+    bool bias_nneg = false;
+};
+
+struct Plan {
+    DevBuf items;
+    int n_items = 0;
+    int subtiles = 1;
+    bool needs_zero = false;
+    int atomics = 0;
+};
+
+using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>;
+
+}  // namespace
+
+struct flm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out, items_tmp;
+    std::map<PlanKey, Plan *> plans;
+    Plan scratch_plan;  // uncached plans (client masking, expansion)
+    int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
+    int table_k = -1;  // seeds in the current device seed table
+};
+
+namespace {
+
+int fail(flm_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_last_error = buf;
+    return code;
+}
+
+#define FLM_HIP(ctx, expr)                                                                            \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail((ctx), FLM_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                    \
+    } while (0)
+
+inline uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
+
+// ------------------------------------------------------------------ planner
+// Split a job into row units (tiles x row parts) and mask units (tiles x seed
+// parts) of equal weight, then pair unit i of each list into one Item, so one
+// workgroup streams rows (HBM) while it generates masks (VALU).
+struct Unit {
+    uint64_t tile;  // out slot of the tile start (relative to job)
+    uint32_t a, n;  // row or seed sub-range
+    uint32_t valid;
+    uint32_t part;
+};
+
+void plan_job(const Job &j, uint64_t pitch, int subtiles, int parts_r, int parts_m, std::vector<Item> &items,
+              bool &needs_zero, int &atomics) {
+    const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
+    std::vector<Unit> R, M;
+    if (j.nrows > 0 && j.L > 0) {
+        for (uint64_t t = 0; t < j.L; t += W)
+            for (int p = 0; p < parts_r; ++p) {
+                uint32_t a = (uint32_t)((uint64_t)j.nrows * p / parts_r);
+                uint32_t b = (uint32_t)((uint64_t)j.nrows * (p + 1) / parts_r);
+                if (b > a) R.push_back({t, a, b - a, (uint32_t)std::min<uint64_t>(W, j.L - t), (uint32_t)p});
+            }
+    }
+    if (j.nseeds > 0 && j.mask_hi > j.mask_lo) {
+        for (uint64_t t = j.mask_lo; t < j.mask_hi; t += W)
+            for (int p = 0; p < parts_m; ++p) {
+                uint32_t a = (uint32_t)((uint64_t)j.nseeds * p / parts_m);
+                uint32_t b = (uint32_t)((uint64_t)j.nseeds * (p + 1) / parts_m);
+                if (b > a)
+                    M.push_back({t, a, b - a, (uint32_t)std::min<uint64_t>(W, j.mask_hi - t), (uint32_t)p});
+            }
+    }
+    // A tile written by exactly one Item is stored; otherwise every contributor
+    // adds atomically into a zeroed output.  Rows and masks share one Item per
+    // tile ("same tile") only in the unsplit whole-vector case.
+    const bool both = !R.empty() && !M.empty();
+    const bool paired_same = both && parts_r == 1 && parts_m == 1 && j.mask_lo == 0 && j.mask_hi == j.L;
+    const bool atomic = parts_r > 1 || parts_m > 1 || (both && !paired_same);
+    if (atomic) needs_zero = true;
+    if (R.empty() && (j.mask_lo > 0 || j.mask_hi < j.L || M.empty())) needs_zero = true;
+    atomics |= atomic ? 1 : 0;
+
+    const size_t n = std::max(R.size(), M.size());
+    for (size_t i = 0; i < n; ++i) {
+        Item it;
+        std::memset(&it, 0, sizeof it);
+        if (i < R.size()) {
+            const Unit &u = R[i];
+            it.flags |= flm::kHasRows | (atomic ? flm::kRowAtomic : 0u);
+            it.row_in = j.rows_base + (uint64_t)u.a * pitch + u.tile;
+            it.nrows = u.n;
+            it.row_out = j.out_base + u.tile;
+            it.row_valid = u.valid;
+        }
+        if (i < M.size()) {
+            const Unit &u = M[i];
+            it.flags |= flm::kHasMask | (atomic ? flm::kMaskAtomic : 0u);
+            it.k0 = j.k0 + u.a;
+            it.nseeds = u.n;
+            it.mask_out = j.out_base + u.tile;
+            it.mask_ctr = (j.prg_slot0 + u.tile) / 16;
+            it.mask_valid = u.valid;
+            if (u.part == 0) {  // per-slot constants are added exactly once
+                it.mask_bias = j.mask_bias;
+                if (j.bias_nneg) it.flags |= flm::kMaskBiasNneg;
+            }
+            if (paired_same && i < R.size() && R[i].tile == u.tile) it.flags |= flm::kSameTile;
+        }
+        items.push_back(it);
+    }
+}
+
+int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t nseeds, int &pr, int &pm) {
+    // Balance mask units against row units, then split both until the grid
+    // has a few workgroups per CU (16 waves each), keeping >= 16 rows/seeds
+    // per item so every wave of a workgroup has work.
+    constexpr uint64_t kTarget = 1024;
+    pr = 1;
+    pm = 1;
+    if (tiles_r && tiles_m && tiles_r > tiles_m) pm = (int)std::min<uint64_t>(nseeds, (tiles_r + tiles_m - 1) / tiles_m);
+    if (tiles_r && tiles_m && tiles_m > tiles_r) pr = (int)std::min<uint64_t>(nrows, (tiles_m + tiles_r - 1) / tiles_r);
+    auto units = [&] { return std::max(tiles_r * pr, tiles_m * pm); };
+    while (units() < kTarget) {
+        bool grew = false;
+        if (tiles_r && (uint64_t)pr * 2 * 16 <= nrows) { pr *= 2; grew = true; }
+        if (tiles_m && (uint64_t)pm * 2 * 16 <= nseeds) { pm *= 2; grew = true; }
+        if (!grew) break;
+    }
+    return 0;
+}
+
+int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
+    plan.n_items = (int)items.size();
+    if (items.empty()) return 0;
+    FLM_HIP(ctx, plan.items.reserve(items.size() * sizeof(Item)));
+    FLM_HIP(ctx, hipMemcpy(plan.items.p, items.data(), items.size() * sizeof(Item), hipMemcpyHostToDevice));
+    return 0;
+}
+
+Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
+                     uint64_t prg_slot0, int *rc) {
+    PlanKey key{0, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
+    auto f = ctx->plans.find(key);
+    if (f != ctx->plans.end()) { *rc = 0; return f->second; }
+    const int subtiles = 1;
+    const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
+    Job j;
+    j.nrows = (uint32_t)N;
+    j.L = L;
+    j.nseeds = (uint32_t)K;
+    j.mask_lo = mask_lo;
+    j.mask_hi = mask_hi;
+    j.prg_slot0 = prg_slot0;
+    j.bias_nneg = true;
+    const uint64_t tr = N > 0 ? (L + W - 1) / W : 0;
+    const uint64_t tm = (K > 0 && mask_hi > mask_lo) ? (mask_hi - mask_lo + W - 1) / W : 0;
+    int pr, pm;
+    choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm);
+    std::vector<Item> items;
+    Plan *plan = new Plan();
+    plan->subtiles = subtiles;
+    plan_job(j, pitch, subtiles, pr, pm, items, plan->needs_zero, plan->atomics);
+    *rc = upload_plan(ctx, *plan, items);
+    if (*rc) { plan->items.release(); delete plan; return nullptr; }
+    if (ctx->plans.size() > 64) {  // bound the cache
+        for (auto &kv : ctx->plans) { kv.second->items.release(); delete kv.second; }
+        ctx->plans.clear();
+    }
+    ctx->plans[key] = plan;
+    return plan;
+}
+
+bool signs_ok(const int8_t *signs, int K, int *nneg) {
+    int n = 0;
+    for (int k = 0; k < K; ++k) {
+        if (signs[k] == -1) ++n;
+        else if (signs[k] != 1) return false;
+    }
+    if (nneg) *nneg = n;
+    return true;
+}
+
+int check_range(flm_ctx *ctx, uint64_t slot_hi) {
+    if (slot_hi > (1ull << 36))
+        return fail(ctx, FLM_ERANGE, "PRG slot range ends at %llu > 2^36 (block counter high word must stay 0)",
+                    (unsigned long long)slot_hi);
+    return 0;
+}
+
+int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s) {
+    FLM_HIP(ctx, ctx->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec)));
+    FLM_HIP(ctx, ctx->meta.reserve(64));
+    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s));
+    ctx->table_k = K;
+    return 0;
+}
+
+int run_plan(flm_ctx *ctx, const Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
+             size_t out_elems, hipStream_t s, int variant) {
+    if (plan.needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
+    FLM_HIP(ctx, flm::launch_items(plan.subtiles, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
+                                   ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
+    ctx->last_items = plan.n_items;
+    ctx->last_tile = flm::kWaveSlots * plan.subtiles;
+    ctx->last_atomics = plan.atomics;
+    ctx->last_variant = variant;
+    return 0;
+}
+
+// Upload N host rows (pageable or pinned) into the context's row buffer at `pitch`.
+int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint64_t pitch) {
+    FLM_HIP(ctx, ctx->rows.reserve(std::max<size_t>(1, (size_t)N) * pitch * sizeof(uint32_t)));
+    for (int i = 0; i < N; ++i) {
+        if (!rows[i]) return fail(ctx, FLM_EINVAL, "row %d is NULL", i);
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->rows.as<uint32_t>() + (size_t)i * pitch, rows[i], L * sizeof(uint32_t),
+                                    hipMemcpyHostToDevice, ctx->stream));
+    }
+    return 0;
+}
+
+int upload_seeds(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K) {
+    FLM_HIP(ctx, ctx->seeds.reserve(std::max<size_t>(1, (size_t)K) * 32));
+    FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
+    if (K > 0) {
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->seeds.p, seeds, (size_t)K * 32, hipMemcpyHostToDevice, ctx->stream));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return 0;
+}
+
+// Client masking / expansion plan: one job per output row, 16 sub-tiles per
+// workgroup (each wave its own 1024 slots, all of the row's seeds).
+// out[i] = (x[i] or base_bias) + sum of row i's seeds (+1 per negative seed).
+int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, const int64_t *seg, const int8_t *signs,
+                  uint32_t base_bias, size_t L, uint64_t slot0, uint32_t *d_out, hipStream_t s, int variant) {
+    const int subtiles = 16;
+    std::vector<Item> items;
+    bool needs_zero = false;
+    int atomics = 0;
+    for (int i = 0; i < N; ++i) {
+        Job j;
+        j.out_base = (uint64_t)i * pitch;
+        j.L = L;
+        const uint32_t k0 = seg ? (uint32_t)seg[i] : (uint32_t)i;
+        const uint32_t k1 = seg ? (uint32_t)seg[i + 1] : (uint32_t)i + 1;
+        uint32_t nneg = 0;
+        if (signs)
+            for (uint32_t k = k0; k < k1; ++k) nneg += signs[k] < 0;
+        const uint32_t bias = (d_x ? 0u : base_bias) + nneg;
+        if (k1 == k0) {
+            // no seeds: out = x (copy) or the constant bias, as a rows-only item
+            const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
+            for (uint64_t t = 0; t < L; t += W) {
+                Item it;
+                std::memset(&it, 0, sizeof it);
+                it.flags = flm::kHasRows;
+                it.row_in = j.out_base + t;
+                it.nrows = d_x ? 1 : 0;
+                it.row_out = j.out_base + t;
+                it.row_valid = (uint32_t)std::min<uint64_t>(W, L - t);
+                it.row_bias = bias;
+                items.push_back(it);
+            }
+            continue;
+        }
+        if (d_x) {
+            j.rows_base = (uint64_t)i * pitch;
+            j.nrows = 1;
+        }
+        j.k0 = k0;
+        j.nseeds = k1 - k0;
+        j.mask_lo = 0;
+        j.mask_hi = L;
+        j.prg_slot0 = slot0;
+        j.mask_bias = bias;
+        plan_job(j, pitch, subtiles, 1, 1, items, needs_zero, atomics);
+    }
+    Plan &plan = ctx->scratch_plan;
+    plan.subtiles = subtiles;
+    plan.needs_zero = needs_zero;
+    plan.atomics = atomics;
+    if (int rc = upload_plan(ctx, plan, items)) return rc;
+    if (needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)N * pitch * sizeof(uint32_t), s));
+    FLM_HIP(ctx, flm::launch_items(subtiles, plan.items.as<Item>(), plan.n_items, d_x, pitch, ctx->recs.as<SeedRec>(),
+                                   ctx->meta.as<uint32_t>(), d_out, s));
+    ctx->last_items = plan.n_items;
+    ctx->last_tile = flm::kWaveSlots * subtiles;
+    ctx->last_atomics = atomics;
+    ctx->last_variant = variant;
+    return 0;
+}
+
+}  // namespace
+
+// ======================================================================= ABI
+extern "C" {
+
+int flm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *flm_version(void) { return "flamingo_hip 0.1 gfx950 items_kernel<S={1,4,16}>"; }
+
+int flm_init(flm_ctx **out, int device) {
+    if (!out) return fail(nullptr, FLM_EINVAL, "flm_init: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(nullptr, FLM_EHIP, "flm_init: no HIP device visible (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) return fail(nullptr, FLM_EINVAL, "flm_init: device %d out of range [0,%d)", device, n);
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(nullptr, FLM_EHIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    flm_ctx *ctx = new flm_ctx();
+    ctx->device = device;
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, FLM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = ctx;
+    return 0;
+}
+
+void flm_free(flm_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->plans) {
+        kv.second->items.release();
+        delete kv.second;
+    }
+    ctx->scratch_plan.items.release();
+    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
+                      &ctx->bytes_out, &ctx->items_tmp})
+        b->release();
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *flm_last_error(const flm_ctx *ctx) {
+    if (ctx) return ctx->err.c_str();
+    return g_last_error.c_str();
+}
+
+int flm_aggregate_unmask(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,
+                         int K, size_t L, uint32_t *out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (N < 0 || K < 0) return fail(ctx, FLM_EINVAL, "negative N or K");
+    if (L == 0) return 0;
+    if (!out || (N > 0 && !rows) || (K > 0 && (!seeds || !signs))) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
+    if (int rc = check_range(ctx, L)) return rc;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t pitch = round_up(L, 64);
+    if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
+    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    FLM_HIP(ctx, ctx->out.reserve(L * sizeof(uint32_t)));
+    if (int rc = flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, N, ctx->seeds.as<uint8_t>(),
+                                          ctx->signs.as<int8_t>(), K, L, 0, L, 0, ctx->out.as<uint32_t>(), ctx->stream))
+        return rc;
+    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->out.p, L * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+static int check_aggregate_args(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L,
+                                size_t mask_lo, size_t mask_hi, uint64_t prg_slot0, const uint32_t *d_out) {
+    if (N < 0 || K < 0) return fail(ctx, FLM_EINVAL, "negative N or K");
+    if (N > 0 && (row_pitch % 4 != 0 || row_pitch < round_up(L, 4)))
+        return fail(ctx, FLM_EINVAL, "row_pitch %zu must be a multiple of 4 and >= round_up(L=%zu, 4)", row_pitch, L);
+    if ((N > 0 && ((uintptr_t)d_rows & 15)) || ((uintptr_t)d_out & 15))
+        return fail(ctx, FLM_EINVAL, "rows and out must be 16-byte aligned");
+    if (mask_hi > L || mask_lo > mask_hi)
+        return fail(ctx, FLM_EINVAL, "mask window [%zu,%zu) outside [0,%zu)", mask_lo, mask_hi, L);
+    if (mask_lo % 16 || prg_slot0 % 16) return fail(ctx, FLM_EINVAL, "mask_lo and prg_slot0 must be multiples of 16");
+    if (int rc = check_range(ctx, prg_slot0 + mask_hi)) return rc;
+    if (N > 0 && !d_rows) return fail(ctx, FLM_EINVAL, "rows is NULL");
+    if (!d_out) return fail(ctx, FLM_EINVAL, "out is NULL");
+    return 0;
+}
+
+int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
+    if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    return run_seed_schedule(ctx, d_seeds, d_signs, K, s);
+}
+
+int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,
+                      size_t mask_hi, uint64_t prg_slot0, uint32_t *d_out, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (L == 0) return 0;
+    if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
+    if (K != ctx->table_k) return fail(ctx, FLM_EINVAL, "K=%d does not match the seed table (%d)", K, ctx->table_k);
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = 0;
+    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
+    if (!plan) return rc;
+    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s, 1);
+}
+
+int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
+                             const int8_t *d_signs, int K, size_t L, size_t mask_lo, size_t mask_hi,
+                             uint64_t prg_slot0, uint32_t *d_out, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (L == 0) return 0;
+    if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
+    if (int rc = flm_seed_table_dev(ctx, d_seeds, d_signs, K, stream)) return rc;
+    return flm_aggregate_dev(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out, stream);
+}
+
+int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,
+                    const int8_t *signs, size_t L, uint32_t *out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (N < 0) return fail(ctx, FLM_EINVAL, "negative N");
+    if (N == 0 || L == 0) return 0;
+    if (!seg || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (seg[0] != 0) return fail(ctx, FLM_EINVAL, "seg[0] must be 0");
+    for (int i = 0; i < N; ++i)
+        if (seg[i + 1] < seg[i]) return fail(ctx, FLM_EINVAL, "seg must be non-decreasing");
+    const int64_t K = seg[N];
+    if (K > 0 && (!seeds || !signs)) return fail(ctx, FLM_EINVAL, "NULL seeds/signs");
+    if (K > 0x7fffffff) return fail(ctx, FLM_EINVAL, "too many seeds");
+    if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
+    if (int rc = check_range(ctx, L)) return rc;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t pitch = round_up(L, 64);
+    uint32_t *d_x = nullptr;
+    if (x) {
+        FLM_HIP(ctx, ctx->rows.reserve((size_t)N * pitch * sizeof(uint32_t)));
+        FLM_HIP(ctx, hipMemcpy2DAsync(ctx->rows.p, pitch * 4, x, L * 4, L * 4, (size_t)N, hipMemcpyHostToDevice,
+                                      ctx->stream));
+        d_x = ctx->rows.as<uint32_t>();
+    }
+    if (int rc = upload_seeds(ctx, seeds, signs, (int)K)) return rc;
+    FLM_HIP(ctx, ctx->out.reserve((size_t)N * pitch * sizeof(uint32_t)));
+    if (int rc = flm_client_mask_dev(ctx, d_x, pitch, N, seg, ctx->seeds.as<uint8_t>(), signs, L, ctx->out.as<uint32_t>(),
+                                     ctx->stream))
+        return rc;
+    FLM_HIP(ctx, hipMemcpy2DAsync(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)N, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, const int64_t *seg,
+                        const uint8_t *d_seeds, const int8_t *signs, size_t L, uint32_t *d_out, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (N <= 0 || L == 0) return 0;
+    if (!seg || !d_out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (pitch % 4 || pitch < round_up(L, 4)) return fail(ctx, FLM_EINVAL, "pitch must be a multiple of 4 and >= L");
+    if (((uintptr_t)d_out & 15) || ((uintptr_t)d_x & 15)) return fail(ctx, FLM_EINVAL, "x/out must be 16-byte aligned");
+    const int64_t K = seg[N];
+    if (K > 0 && (!d_seeds || !signs)) return fail(ctx, FLM_EINVAL, "NULL seeds/signs");
+    if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
+    if (int rc = check_range(ctx, L)) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    // signs go to the device with the seeds (the schedule folds them into xorc)
+    FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
+    if (K > 0) FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, s));
+    if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), (int)K, s)) return rc;
+    return run_rows_jobs(ctx, d_x, pitch, N, seg, signs, 1u, L, 0, d_out, s, 2);
+}
+
+int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t slot0, uint32_t *out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
+    if (K == 0 || L == 0) return 0;
+    if (!seeds || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (slot0 % 16) return fail(ctx, FLM_EINVAL, "slot0 must be a multiple of 16");
+    if (int rc = check_range(ctx, slot0 + L)) return rc;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t pitch = round_up(L, 64);
+    FLM_HIP(ctx, ctx->seeds.reserve((size_t)K * 32));
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->seeds.p, seeds, (size_t)K * 32, hipMemcpyHostToDevice, ctx->stream));
+    FLM_HIP(ctx, ctx->out.reserve((size_t)K * pitch * sizeof(uint32_t)));
+    if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, ctx->out.as<uint32_t>(), pitch,
+                                    ctx->stream))
+        return rc;
+    FLM_HIP(ctx, hipMemcpy2DAsync(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)K, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, uint64_t slot0, uint32_t *d_out,
+                       size_t pitch, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (K <= 0 || L == 0) return 0;
+    if (slot0 % 16) return fail(ctx, FLM_EINVAL, "slot0 must be a multiple of 16");
+    if (pitch % 4 || pitch < round_up(L, 4)) return fail(ctx, FLM_EINVAL, "pitch must be a multiple of 4 and >= L");
+    if ((uintptr_t)d_out & 15) return fail(ctx, FLM_EINVAL, "out must be 16-byte aligned");
+    if (int rc = check_range(ctx, slot0 + L)) return rc;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<int8_t> plus((size_t)K, 1);
+    FLM_HIP(ctx, ctx->signs.reserve((size_t)K));
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, plus.data(), (size_t)K, hipMemcpyHostToDevice, s));
+    if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), K, s)) return rc;
+    // the staging vector must outlive the async copy
+    FLM_HIP(ctx, hipStreamSynchronize(s));
+    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, 0u, L, slot0, d_out, s, 3);
+}
+
+int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *acc, size_t L,
+                        uint64_t slot0) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
+    if (L == 0) return 0;
+    if (!acc || (K > 0 && (!seeds || !signs))) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (slot0 % 16) return fail(ctx, FLM_EINVAL, "slot0 must be a multiple of 16");
+    if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
+    if (int rc = check_range(ctx, slot0 + L)) return rc;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t pitch = round_up(L, 64);
+    FLM_HIP(ctx, ctx->rows.reserve(pitch * sizeof(uint32_t)));
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->rows.p, acc, L * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    FLM_HIP(ctx, ctx->out.reserve(pitch * sizeof(uint32_t)));
+    if (int rc = flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, 1, ctx->seeds.as<uint8_t>(),
+                                          ctx->signs.as<int8_t>(), K, L, 0, L, slot0, ctx->out.as<uint32_t>(),
+                                          ctx->stream))
+        return rc;
+    FLM_HIP(ctx, hipMemcpyAsync(acc, ctx->out.p, L * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8], uint64_t counter, const uint8_t *in,
+                     uint8_t *out, size_t n) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (n == 0) return 0;
+    if (!key || !nonce || !in || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    uint32_t k[8], nn[2];
+    for (int i = 0; i < 8; ++i)
+        k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+               ((uint32_t)key[4 * i + 3] << 24);
+    for (int i = 0; i < 2; ++i)
+        nn[i] = (uint32_t)nonce[4 * i] | ((uint32_t)nonce[4 * i + 1] << 8) | ((uint32_t)nonce[4 * i + 2] << 16) |
+                ((uint32_t)nonce[4 * i + 3] << 24);
+    FLM_HIP(ctx, ctx->bytes_in.reserve(n));
+    FLM_HIP(ctx, ctx->bytes_out.reserve(n));
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->bytes_in.p, in, n, hipMemcpyHostToDevice, ctx->stream));
+    FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, ctx->bytes_in.as<uint8_t>(), ctx->bytes_out.as<uint8_t>(), n,
+                                          ctx->stream));
+    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->bytes_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flm_check_signs(flm_ctx *ctx, int *bad_count) {
+    if (!ctx || !bad_count) return fail(ctx, FLM_EINVAL, "NULL argument");
+    uint32_t meta[2] = {0, 0};
+    if (!ctx->meta.p) { *bad_count = 0; return 0; }
+    FLM_HIP(ctx, hipMemcpy(meta, ctx->meta.p, sizeof meta, hipMemcpyDeviceToHost));
+    *bad_count = (int)meta[1];
+    return 0;
+}
+
+int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics, int *variant) {
+    if (!ctx) return FLM_EINVAL;
+    if (items) *items = ctx->last_items;
+    if (tile_slots) *tile_slots = ctx->last_tile;
+    if (atomics) *atomics = ctx->last_atomics;
+    if (variant) *variant = ctx->last_variant;
+    return 0;
+}
+
+void *flm_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void flm_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+"""Multi-GPU server round: client-sharded rows, slot-sharded unmask, RCCL reduce-scatter.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
+ROCm).  Rank r of G holds the masked vectors of its own clients (the VECTOR
+bodies it ingested over its own PCIe link) and owns slot shard
+[r*S, (r+1)*S) of the output, S = Lp / G with Lp = L rounded up to 1024*G:
+
+  partial_r[l] = sum_{i in clients(r)} y_i[l]                    l in [0, L)
+               + sum_k sign_k * PRG(seed_k)[l]                   l in shard(r)
+  out_r        = reduce_scatter_sum(partial_0..G-1)[shard(r)]
+
+The mask term is added by exactly one rank per slot, so the reduce-scatter
+returns S + C + M of SA_ServiceAgent.py:605 for that shard.  Integer addition
+is associative and commutative mod 2^32, so every ring order gives the same
+bits.  Each rank regenerates all K masks but only over its own slots, which
+splits the VALU-bound ChaCha work G ways; the row sum (HBM-bound) is split by
+clients.  The only collective is one reduce-scatter of Lp*4 bytes per round.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+SHARD_ALIGN = 1024  # a wave's sub-tile; keeps every shard start a multiple of 16 slots
+
+
+def padded_length(L: int, world: int) -> int:
+    q = SHARD_ALIGN * world
+    return (L + q - 1) // q * q
+
+
+def shard_bounds(L: int, world: int, rank: int):
+    """[lo, hi) of output slots owned by `rank` (hi clipped to L; may be empty)."""
+    S = padded_length(L, world) // world
+    lo = min(rank * S, L)
+    hi = min((rank + 1) * S, L)
+    return lo, hi
+
+
+def client_bounds(N: int, world: int, rank: int):
+    """Contiguous block of clients ingested by `rank`."""
+    return N * rank // world, N * (rank + 1) // world
+
+
+class ShardedRound:
+    """Runs one rank's share of a round on its GPU and reduce-scatters the partials."""
+
+    def __init__(self, engine, L: int, group=None):
+        self.engine = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.L = L
+        self.Lp = padded_length(L, self.world)
+        self.lo, self.hi = shard_bounds(L, self.world, self.rank)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.partial = torch.zeros(self.Lp, dtype=torch.int32, device=dev)
+        self.out = torch.empty(self.Lp // self.world, dtype=torch.int32, device=dev)
+
+    def prepare_seeds(self, d_seeds, d_signs, stream=None):
+        self.K = d_seeds.shape[0]
+        self.engine.seed_table_dev(d_seeds, d_signs, stream=stream)
+
+    def compute(self, d_rows, stream=None):
+        """Row sum over all slots + unmask over this rank's shard (one kernel)."""
+        self.engine.aggregate_dev(d_rows, self.K, self.partial, L=self.L, mask_lo=self.lo, mask_hi=self.hi,
+                                  stream=stream)
+
+    def exchange(self):
+        if self.world == 1:
+            return self.partial[: self.L]
+        dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM, group=self.group)
+        return self.out[: self.hi - self.lo]
+
+    def step(self, d_rows, d_seeds, d_signs, stream=None):
+        self.prepare_seeds(d_seeds, d_signs, stream)
+        self.compute(d_rows, stream)
+        return self.exchange()

@@ -1,0 +1,280 @@
+"""Host-side handle on the MI355X engine (libflamingo_hip.so).
+
+``MaskEngine`` owns one C-ABI context bound to one GPU (one process per GPU).
+Its methods are the calls the drop-in agents make in place of the reference's
+numpy/pycryptodomex loops:
+
+* ``aggregate_unmask`` -- SA_ServiceAgent.report_process partial sum
+  (agent/flamingo/SA_ServiceAgent.py:346-350) + reconstruction_process unmask
+  and combine (:529-540, :587-605).
+* ``client_mask`` -- SA_ClientAgent.sendVectors mask composition
+  (agent/flamingo/SA_ClientAgent.py:246-324), batched over clients.
+* ``prg_expand`` / ``prg`` -- the PRG idiom ChaCha20(seed).encrypt(b"abcd"*L)
+  viewed as uint32 (SA_ClientAgent.py:248-250).
+* ``chacha20_encrypt`` -- ChaCha20.new(key, nonce).encrypt(data) for the
+  PRF/PRG calls of util/param.py:44-46, 63-76.
+* ``*_dev`` -- the same on device-resident torch tensors (bench, multi-GPU).
+
+Errors surface as RuntimeError with the library's message, like the
+reference's own guards (SA_ServiceAgent.py:349, 502).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import p_i8, p_i64, p_u8, p_u32
+
+NONCE = b"\x00" * 8
+
+
+def _seeds_array(seeds) -> np.ndarray:
+    if isinstance(seeds, (list, tuple)):
+        if len(seeds) == 0:
+            return np.zeros((0, 32), np.uint8)
+        if isinstance(seeds[0], (bytes, bytearray)):
+            if any(len(s) != 32 for s in seeds):
+                raise RuntimeError("every seed must be 32 bytes")
+            return np.frombuffer(b"".join(bytes(s) for s in seeds), dtype=np.uint8).reshape(-1, 32).copy()
+    a = np.ascontiguousarray(seeds, dtype=np.uint8)
+    if a.size % 32:
+        raise RuntimeError("seeds must be K x 32 bytes")
+    return a.reshape(-1, 32)
+
+
+def _signs_array(signs, K: int) -> np.ndarray:
+    s = np.ascontiguousarray(signs, dtype=np.int8).reshape(-1)
+    if s.shape[0] != K:
+        raise RuntimeError(f"{s.shape[0]} signs for {K} seeds")
+    return s
+
+
+class MaskEngine:
+    """One GPU's mask-and-aggregate engine (a flm_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        self.device = device
+        ctx = ctypes.c_void_p()
+        rc = self.lib.flm_init(ctypes.byref(ctx), device)
+        if rc != 0:
+            raise RuntimeError(f"flm_init(device={device}) failed: {self.lib.flm_last_error(None).decode()}")
+        self.ctx = ctx
+
+    # ------------------------------------------------------------ plumbing
+    def close(self):
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self.lib.flm_free(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.flm_last_error(self.ctx).decode()} (code {rc})")
+
+    def last_plan(self) -> dict:
+        v = [ctypes.c_int() for _ in range(4)]
+        self.lib.flm_last_plan(self.ctx, *[ctypes.byref(x) for x in v])
+        return {"items": v[0].value, "tile_slots": v[1].value, "atomics": v[2].value, "variant": v[3].value}
+
+    # -------------------------------------------------------- host arrays
+    def aggregate_unmask(self, vectors, seeds, signs, L: int | None = None) -> np.ndarray:
+        """sum(vectors) + sum_k signs[k]*PRG(seeds[k]) mod 2^32 (host in, host out).
+
+        vectors: a list of uint32 arrays (the VECTOR bodies) or an (N, L) array."""
+        if isinstance(vectors, np.ndarray) and vectors.ndim == 2:
+            rows = [np.ascontiguousarray(vectors[i], dtype=np.uint32) for i in range(vectors.shape[0])]
+        else:
+            rows = [np.ascontiguousarray(v, dtype=np.uint32) for v in vectors]
+        if L is None:
+            if not rows:
+                raise RuntimeError("L is required when there are no vectors")
+            L = rows[0].shape[0]
+        for v in rows:
+            if v.shape[0] != L:
+                raise RuntimeError("Client sends vector of incorrect length.")  # SA_ServiceAgent.py:348-349
+        seeds = _seeds_array(seeds)
+        signs = _signs_array(signs, seeds.shape[0])
+        out = np.empty(L, dtype=np.uint32)
+        ptrs = (_lib._u32p * max(1, len(rows)))(*[p_u32(v) for v in rows])
+        rc = self.lib.flm_aggregate_unmask(self.ctx, ptrs, len(rows), p_u8(seeds), p_i8(signs), seeds.shape[0],
+                                           L, p_u32(out))
+        self._check(rc, "flm_aggregate_unmask")
+        return out
+
+    def client_mask(self, seg, seeds, signs, L: int, x: np.ndarray | None = None) -> np.ndarray:
+        """y_i = x_i (or ones) + sum_{k in seg i} signs[k]*PRG(seeds[k]); returns (N, L) uint32."""
+        seg = np.ascontiguousarray(seg, dtype=np.int64)
+        N = seg.shape[0] - 1
+        seeds = _seeds_array(seeds)
+        signs = _signs_array(signs, seeds.shape[0])
+        if seg[-1] != seeds.shape[0]:
+            raise RuntimeError("seg[-1] must equal the number of seeds")
+        out = np.empty((N, L), dtype=np.uint32)
+        xp = None
+        if x is not None:
+            x = np.ascontiguousarray(x, dtype=np.uint32)
+            if x.shape != (N, L):
+                raise RuntimeError("x must be (N, L)")
+            xp = p_u32(x)
+        rc = self.lib.flm_client_mask(self.ctx, xp, N, p_i64(seg), p_u8(seeds), p_i8(signs), L, p_u32(out))
+        self._check(rc, "flm_client_mask")
+        return out
+
+    def prg_expand(self, seeds, L: int, slot0: int = 0) -> np.ndarray:
+        """PRG(seed_k)[slot0:slot0+L] for every seed; (K, L) uint32."""
+        seeds = _seeds_array(seeds)
+        out = np.empty((seeds.shape[0], L), dtype=np.uint32)
+        rc = self.lib.flm_prg_expand(self.ctx, p_u8(seeds), seeds.shape[0], L, slot0, p_u32(out))
+        self._check(rc, "flm_prg_expand")
+        return out
+
+    def prg(self, seed: bytes, L: int, slot0: int = 0) -> np.ndarray:
+        return self.prg_expand([seed], L, slot0)[0]
+
+    def mask_accumulate(self, seeds, signs, acc: np.ndarray, slot0: int = 0) -> np.ndarray:
+        """acc += sum_k signs[k]*PRG(seeds[k])[slot0:] in place; returns acc."""
+        if acc.dtype != np.uint32 or not acc.flags.c_contiguous:
+            raise RuntimeError("acc must be a C-contiguous uint32 array")
+        seeds = _seeds_array(seeds)
+        signs = _signs_array(signs, seeds.shape[0])
+        rc = self.lib.flm_mask_accumulate(self.ctx, p_u8(seeds), p_i8(signs), seeds.shape[0], p_u32(acc),
+                                          acc.shape[0], slot0)
+        self._check(rc, "flm_mask_accumulate")
+        return acc
+
+    def chacha20_encrypt(self, key: bytes, data: bytes, nonce: bytes = NONCE, counter: int = 0) -> bytes:
+        """ChaCha20.new(key=key, nonce=nonce).encrypt(data) (DJB layout), on the GPU."""
+        if len(key) != 32 or len(nonce) != 8:
+            raise RuntimeError("key must be 32 bytes and nonce 8 bytes")
+        n = len(data)
+        if n == 0:
+            return b""
+        src = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        dst = np.empty(n, dtype=np.uint8)
+        k = np.frombuffer(bytes(key), dtype=np.uint8).copy()
+        nn = np.frombuffer(bytes(nonce), dtype=np.uint8).copy()
+        rc = self.lib.flm_chacha20_xor(self.ctx, p_u8(k), p_u8(nn), counter, p_u8(src), p_u8(dst), n)
+        self._check(rc, "flm_chacha20_xor")
+        return dst.tobytes()
+
+    # ------------------------------------------------------ device tensors
+    @staticmethod
+    def _stream_handle(stream):
+        if stream is None:
+            import torch
+            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        if isinstance(stream, int):
+            return ctypes.c_void_p(stream)
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    def aggregate_unmask_dev(self, rows, seeds, signs, out, L: int | None = None, mask_lo: int = 0,
+                             mask_hi: int | None = None, prg_slot0: int = 0, stream=None):
+        """Enqueue the device-resident round on `stream` (default: torch's current stream).
+
+        rows: (N, pitch) int32/uint32 CUDA tensor (pitch % 4 == 0, pitch >= L);
+        seeds: (K, 32) uint8 CUDA tensor; signs: (K,) int8 CUDA tensor;
+        out: CUDA tensor with >= L int32/uint32 elements."""
+        N = rows.shape[0] if rows is not None else 0
+        pitch = rows.shape[1] if N else 0
+        if L is None:
+            L = pitch
+        if mask_hi is None:
+            mask_hi = L
+        K = seeds.shape[0] if seeds is not None else 0
+        rc = self.lib.flm_aggregate_unmask_dev(
+            self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N,
+            ctypes.c_void_p(seeds.data_ptr() if K else 0), ctypes.c_void_p(signs.data_ptr() if K else 0), K, L,
+            mask_lo, mask_hi, prg_slot0, ctypes.c_void_p(out.data_ptr()), self._stream_handle(stream))
+        self._check(rc, "flm_aggregate_unmask_dev")
+        return out
+
+    def seed_table_dev(self, seeds, signs, stream=None):
+        """Build the device seed schedule (first of the round's two launches)."""
+        K = seeds.shape[0] if seeds is not None else 0
+        rc = self.lib.flm_seed_table_dev(self.ctx, ctypes.c_void_p(seeds.data_ptr() if K else 0),
+                                         ctypes.c_void_p(signs.data_ptr() if K else 0), K,
+                                         self._stream_handle(stream))
+        self._check(rc, "flm_seed_table_dev")
+
+    def aggregate_dev(self, rows, K: int, out, L: int | None = None, mask_lo: int = 0, mask_hi: int | None = None,
+                      prg_slot0: int = 0, stream=None):
+        """Row-sum + unmask kernel against the current seed table (second launch)."""
+        N = rows.shape[0] if rows is not None else 0
+        pitch = rows.shape[1] if N else 0
+        if L is None:
+            L = pitch
+        if mask_hi is None:
+            mask_hi = L
+        rc = self.lib.flm_aggregate_dev(self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N, K, L,
+                                        mask_lo, mask_hi, prg_slot0, ctypes.c_void_p(out.data_ptr()),
+                                        self._stream_handle(stream))
+        self._check(rc, "flm_aggregate_dev")
+        return out
+
+    def client_mask_dev(self, seg, seeds_dev, signs, out, L: int, x=None, stream=None):
+        """Device client masking: seg/signs host arrays, seeds_dev/x/out CUDA tensors (rows at out.shape[1])."""
+        seg = np.ascontiguousarray(seg, dtype=np.int64)
+        N = seg.shape[0] - 1
+        signs = np.ascontiguousarray(signs, dtype=np.int8)
+        pitch = out.shape[1]
+        rc = self.lib.flm_client_mask_dev(self.ctx, ctypes.c_void_p(x.data_ptr() if x is not None else 0), pitch, N,
+                                          p_i64(seg), ctypes.c_void_p(seeds_dev.data_ptr()), p_i8(signs), L,
+                                          ctypes.c_void_p(out.data_ptr()), self._stream_handle(stream))
+        self._check(rc, "flm_client_mask_dev")
+        return out
+
+    def prg_expand_dev(self, seeds_dev, out, L: int, slot0: int = 0, stream=None):
+        K = seeds_dev.shape[0]
+        rc = self.lib.flm_prg_expand_dev(self.ctx, ctypes.c_void_p(seeds_dev.data_ptr()), K, L, slot0,
+                                         ctypes.c_void_p(out.data_ptr()), out.shape[1], self._stream_handle(stream))
+        self._check(rc, "flm_prg_expand_dev")
+        return out
+
+    def check_signs(self) -> int:
+        bad = ctypes.c_int()
+        self._check(self.lib.flm_check_signs(self.ctx, ctypes.byref(bad)), "flm_check_signs")
+        return bad.value
+
+
+class PinnedArena:
+    """Page-locked host memory (hipHostMalloc) viewed as numpy arrays.
+
+    Client vectors allocated here reach the GPU by DMA at the full PCIe rate
+    (the reference keeps them as pageable numpy arrays, SA_ServiceAgent.py:210)."""
+
+    def __init__(self, nbytes: int):
+        self.lib = _lib.load()
+        self.ptr = self.lib.flm_host_alloc(nbytes)
+        if not self.ptr:
+            raise RuntimeError(f"flm_host_alloc({nbytes}) failed")
+        self.nbytes = nbytes
+        self.off = 0
+
+    def array(self, shape, dtype=np.uint32) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        off = (self.off + 255) // 256 * 256
+        if off + n > self.nbytes:
+            raise RuntimeError("pinned arena exhausted")
+        self.off = off + n
+        buf = (ctypes.c_uint8 * n).from_address(self.ptr + off)
+        return np.frombuffer(buf, dtype=dt).reshape(shape)
+
+    def free(self):
+        if self.ptr:
+            self.lib.flm_host_free(self.ptr)
+            self.ptr = None

@@ -1,0 +1,150 @@
+/*
+ * flamingo_hip.h -- C ABI of libflamingo_hip.so, the MI355X (gfx950) engine
+ * behind Flamingo's per-round mask-and-aggregate path.
+ *
+ * The reference (eniac/flamingo, pure Python) has no FFI; these entry points
+ * replace the bodies of the reference's hot loops under an unchanged agent
+ * surface.  Each function cites the reference code it stands in for
+ * (paths relative to the reference root).
+ *
+ * Arithmetic: uint32 mod 2^32 everywhere (util/param.py:9 vector_type).
+ * PRG(seed)[l] = LE32(ChaCha20_DJB(key=seed, nonce=0^8).keystream[4l:4l+4])
+ *                ^ 0x64636261 (b"abcd", util/param.py:12,32).
+ *
+ * Conventions
+ *  - Return 0 on success, a negative FLM_E* code on failure; the message is
+ *    available from flm_last_error(ctx) (or flm_last_error(NULL) when no
+ *    context could be created).  The Python layer raises RuntimeError, as the
+ *    reference does on its own guard failures (SA_ServiceAgent.py:349,502).
+ *  - seeds are K x 32 bytes (the reference's 32-byte ChaCha20 keys:
+ *    m_i.to_bytes(32,'big') at SA_ServiceAgent.py:526, SHA-256 digests at
+ *    :583-585); signs are K int8 in {+1,-1} (recon_symbol, :375-378; self
+ *    masks are always -1, :536).
+ *  - Host-pointer functions are synchronous: they copy in, compute on the
+ *    GPU and copy out; no host pointer is retained after return.
+ *  - *_dev functions take device pointers and enqueue work on `stream`
+ *    (a hipStream_t; NULL = the context's own stream) without synchronising.
+ *  - One context per host thread; a context binds one GPU (one process per
+ *    GPU).  Create it lazily, after any fork (SA_ServiceAgent.py:562 forks a
+ *    multiprocessing.Pool).
+ */
+#ifndef FLAMINGO_HIP_H
+#define FLAMINGO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLM_OK 0
+#define FLM_EINVAL (-1)   /* bad argument (length mismatch, sign not +-1, alignment) */
+#define FLM_EHIP (-2)     /* HIP runtime error */
+#define FLM_ENOMEM (-3)   /* device or pinned allocation failed */
+#define FLM_ERANGE (-4)   /* slot range beyond 2^36 (block counter high word must be 0) */
+
+typedef struct flm_ctx flm_ctx;
+
+/* ------------------------------------------------------------ lifecycle */
+int flm_device_count(void);
+/* Bind a context to HIP device `device` and create its stream. */
+int flm_init(flm_ctx **out, int device);
+void flm_free(flm_ctx *ctx);
+const char *flm_last_error(const flm_ctx *ctx);
+/* Library / kernel build identification string (static storage). */
+const char *flm_version(void);
+
+/* ---------------------------------------------------- host-memory path */
+
+/* Server round: replaces SA_ServiceAgent.report_process's partial sum
+ * (agent/flamingo/SA_ServiceAgent.py:346-350) and reconstruction_process's
+ * self-mask and dropout-pair unmask + final combine (:529-540, :587-605):
+ *   out[l] = sum_{i<N} rows[i][l] + sum_{k<K} signs[k] * PRG(seeds[k])[l]
+ * rows: N host pointers to L uint32 each (the VECTOR bodies, :210). */
+int flm_aggregate_unmask(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds,
+                         const int8_t *signs, int K, size_t L, uint32_t *out);
+
+/* Client masking, batched over N clients: replaces SA_ClientAgent.sendVectors's
+ * mask expansion and composition (agent/flamingo/SA_ClientAgent.py:246-324):
+ *   out[i][l] = x[i][l] + sum_{k in [seg[i], seg[i+1])} signs[k] * PRG(seeds[k])[l]
+ * x: N x L row-major uint32, or NULL for the reference's all-ones input (:304).
+ * out: N x L row-major. */
+int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,
+                    const int8_t *signs, size_t L, uint32_t *out);
+
+/* Standalone PRG expansion: out[k][l] = PRG(seeds[k])[slot0 + l], K x L
+ * row-major (the idiom at SA_ClientAgent.py:248-250 / SA_ServiceAgent.py:533-535
+ * for a whole batch).  slot0 must be a multiple of 16. */
+int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t slot0, uint32_t *out);
+
+/* acc[l] += sum_k signs[k] * PRG(seeds[k])[slot0 + l], in place on a host
+ * vector (the mi_vec / cancel_vec loops, SA_ServiceAgent.py:530-536, 595-603,
+ * on a slot window).  slot0 must be a multiple of 16. */
+int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *acc,
+                        size_t L, uint64_t slot0);
+
+/* ChaCha20(key, nonce).encrypt(in) from block `counter` on, byte-exact, any
+ * length: the PRF/PRG calls of util/param.py:44-46 (choose_committee) and
+ * :63-76 (findNeighbors), computed on the GPU. */
+int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8], uint64_t counter,
+                     const uint8_t *in, uint8_t *out, size_t n);
+
+/* -------------------------------------------------- device-resident path */
+
+/* Device-resident server round over a slot window, for single- and multi-GPU use:
+ *   out[l]  = sum_{i<N} rows[i*row_pitch + l]                  for l in [0, L)
+ *           + sum_k signs[k] * PRG(seeds[k])[prg_slot0 + l]    for l in [mask_lo, mask_hi)
+ * (mod 2^32).  With mask_lo=0, mask_hi=L, prg_slot0=0 this is the whole
+ * round; on G GPUs each rank passes its own client rows and its own slot
+ * shard [mask_lo, mask_hi) and the partial vectors are then reduce-scattered.
+ * Requirements: row_pitch % 4 == 0 and row_pitch >= round_up(L, 4);
+ * rows and out 16-byte aligned; mask_lo % 16 == 0; prg_slot0 % 16 == 0;
+ * prg_slot0 + mask_hi <= 2^36.  d_seeds: K x 32 bytes, d_signs: K int8 (+-1).
+ * Enqueued on `stream`; nothing is synchronised. */
+int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N,
+                             const uint8_t *d_seeds, const int8_t *d_signs, int K, size_t L,
+                             size_t mask_lo, size_t mask_hi, uint64_t prg_slot0, uint32_t *d_out,
+                             void *stream);
+
+/* The same round split in its two launches, so a caller can time the
+ * dominant kernel alone: flm_seed_table_dev builds the context's per-seed
+ * schedule (ChaCha key words, sign, counter-independent first-round words)
+ * from device seeds/signs; flm_aggregate_dev then runs the row-sum + unmask
+ * kernel against that table (K must match the table).  Same requirements as
+ * flm_aggregate_unmask_dev. */
+int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, void *stream);
+int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L,
+                      size_t mask_lo, size_t mask_hi, uint64_t prg_slot0, uint32_t *d_out, void *stream);
+
+/* Device-resident client masking (flm_client_mask on device buffers).  seg and
+ * signs are host arrays (they size the launch); seeds, x and out are device
+ * pointers; x may be NULL (all-ones input).  x and out rows use `pitch`. */
+int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, const int64_t *seg,
+                        const uint8_t *d_seeds, const int8_t *signs, size_t L, uint32_t *d_out,
+                        void *stream);
+
+/* Device-resident PRG expansion: d_out[k*pitch + l] = PRG(seed k)[slot0 + l]. */
+int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, uint64_t slot0,
+                       uint32_t *d_out, size_t pitch, void *stream);
+
+/* After a *_dev call has completed on its stream: number of signs that were
+ * not +-1 in the last seed table (0 when valid). */
+int flm_check_signs(flm_ctx *ctx, int *bad_count);
+
+/* ----------------------------------------------------------- diagnostics */
+
+/* Describe the launch plan the last *aggregate* call used:
+ * items, tile slots, atomics used (0/1), kernel variant id. */
+int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics, int *variant);
+
+/* Allocate / free page-locked host memory through HIP (for a pinned arena
+ * holding client vectors, so host->device copies are DMA at full PCIe rate). */
+void *flm_host_alloc(size_t bytes);
+void flm_host_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLAMINGO_HIP_H */

@@ -1,0 +1,227 @@
+"""Parity of the HIP path (through the C ABI) against the CPU oracle and the
+OpenSSL-generated golden fixtures.  Bit-exact: this is uint32 arithmetic.
+
+Edge cases follow what the reference's path can see: lengths that are not
+multiples of a ChaCha block (default vector_len 16000, util/param.py:8), no
+dropouts (K = |U|, SA_ServiceAgent.py:538-540), dropouts with both signs
+(:375-378), mod-2^32 wrap, empty sets, and the full benchmark size through
+the out == |U| invariant (SA_ClientAgent.py:304 + SA_ServiceAgent.py:605).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def h(v):
+    return hashlib.sha256(np.ascontiguousarray(v, dtype="<u4").tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from flamingo_amd import MaskEngine
+    e = MaskEngine(0)
+    yield e
+    e.close()
+
+
+def rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def rand_case(seed, N, K, L):
+    g = rng(seed)
+    rows = g.integers(0, 2**32, size=(N, L), dtype=np.uint32)
+    seeds = g.integers(0, 256, size=(K, 32), dtype=np.uint8)
+    signs = np.where(g.random(K) < 0.5, 1, -1).astype(np.int8)
+    return rows, seeds, signs
+
+
+# ------------------------------------------------------------------ PRG
+def test_prg_golden(eng, golden):
+    by_seed = {}
+    for e in golden["prg"]:
+        by_seed.setdefault(e["seed"], []).append(e)
+    for seed_hex, entries in by_seed.items():
+        seed = bytes.fromhex(seed_hex)
+        for e in entries:
+            v = eng.prg(seed, e["L"])
+            assert v[:32].tolist() == e["head"], (e["name"], e["L"])
+            assert h(v) == e["sha256"], (e["name"], e["L"])
+
+
+def test_prg_windows_golden(eng, golden):
+    for e in golden["prg_windows"]:
+        seed = bytes.fromhex(e["seed"])
+        if e["slot0"] % 16:
+            continue
+        v = eng.prg(seed, e["n"], slot0=e["slot0"])
+        assert h(v) == e["sha256"], (e["slot0"], e["n"])
+
+
+def test_prg_expand_batch_vs_oracle(eng):
+    g = rng(11)
+    seeds = g.integers(0, 256, size=(37, 32), dtype=np.uint8)
+    for L in (1, 15, 16, 17, 1000, 1023, 1024, 1025, 16000, 16385, 40000):
+        got = eng.prg_expand(seeds, L)
+        for k in (0, 1, 17, 36):
+            assert np.array_equal(got[k], O.prg(seeds[k].tobytes(), L)), (k, L)
+
+
+def test_keystream_golden(eng, golden):
+    for e in golden["keystream"]:
+        key, data = bytes.fromhex(e["key"]), bytes.fromhex(e["data"])
+        assert eng.chacha20_encrypt(key, data).hex() == e["ct"]
+    # arbitrary nonce / counter against the oracle
+    key = bytes(range(32))
+    data = bytes(rng(5).integers(0, 256, 1000, dtype=np.uint8))
+    nonce = bytes.fromhex("0000004a00000000")
+    assert eng.chacha20_encrypt(key, data, nonce, counter=7) == O.chacha20_encrypt(key, data, nonce, counter=7)
+
+
+# ------------------------------------------------------------- client side
+def test_client_mask_round_n128(eng, golden, round128):
+    g, r = golden["round_n128"], round128
+    rows = eng.client_mask(r["client_seg"], r["client_seeds"], r["client_signs"], g["L"])
+    assert rows[:4, :8].tolist() == g["rows_head"]
+    assert h(rows) == g["rows_sha256"]
+    x = rng(20231015).integers(0, 2**32, size=(128, g["L"]), dtype=np.uint32)
+    rows_x = eng.client_mask(r["client_seg"], r["client_seeds"], r["client_signs"], g["L"], x=x)
+    assert h(rows_x) == g["rows_x_sha256"]
+
+
+def test_client_mask_ragged_vs_oracle(eng):
+    g = rng(3)
+    N, L = 9, 2077
+    deg = g.integers(0, 5, size=N)          # includes clients with no pairwise seeds
+    seg = np.concatenate([[0], np.cumsum(deg + 1)]).astype(np.int64)
+    K = int(seg[-1])
+    seeds = g.integers(0, 256, size=(K, 32), dtype=np.uint8)
+    signs = np.where(g.random(K) < 0.5, 1, -1).astype(np.int8)
+    want = O.client_mask(seg, seeds, signs, L)
+    assert np.array_equal(eng.client_mask(seg, seeds, signs, L), want)
+    x = g.integers(0, 2**32, size=(N, L), dtype=np.uint32)
+    assert np.array_equal(eng.client_mask(seg, seeds, signs, L, x=x), O.client_mask(seg, seeds, signs, L, x=x))
+    # a client with no seeds at all
+    seg0 = np.array([0, 0, 2], np.int64)
+    got = eng.client_mask(seg0, seeds[:2], signs[:2], 100)
+    assert np.all(got[0] == 1)
+    assert np.array_equal(got, O.client_mask(seg0, seeds[:2], signs[:2], 100))
+
+
+# ------------------------------------------------------------- server side
+def test_round_n128_server(eng, golden, round128):
+    g, r = golden["round_n128"], round128
+    rows = O.client_mask(r["client_seg"], r["client_seeds"], r["client_signs"], g["L"])
+    online = r["online"]
+    vectors = [rows[i] for i in online]
+    out = eng.aggregate_unmask(vectors, r["server_seeds"], r["server_signs"])
+    assert np.all(out == g["final_value"])
+    x = rng(20231015).integers(0, 2**32, size=(128, g["L"]), dtype=np.uint32)
+    rows_x = O.client_mask(r["client_seg"], r["client_seeds"], r["client_signs"], g["L"], x=x)
+    out_x = eng.aggregate_unmask(rows_x[online], r["server_seeds"], r["server_signs"])
+    assert h(out_x) == g["final_x_sha256"]
+
+
+@pytest.mark.parametrize("N,K,L", [
+    (1, 1, 1), (3, 2, 17), (5, 0, 1000), (0, 7, 1000), (128, 128, 16000), (128, 158, 16384),
+    (64, 3, 16385), (17, 300, 4099), (1, 1, 65536), (200, 13, 2**18 + 48), (2, 0, 5), (33, 33, 1024),
+])
+def test_aggregate_vs_oracle(eng, N, K, L):
+    rows, seeds, signs = rand_case(N * 1000 + K * 10 + L, N, K, L)
+    want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+    got = eng.aggregate_unmask(list(rows), seeds, signs, L=L)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+
+
+def test_aggregate_wraps_mod_2_32(eng):
+    rows = np.full((7, 333), 0xFFFFFFFF, np.uint32)
+    out = eng.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8))
+    assert np.all(out == np.uint32((7 * 0xFFFFFFFF) % 2**32))
+
+
+def test_mask_accumulate_windows(eng):
+    g = rng(9)
+    seeds = g.integers(0, 256, size=(5, 32), dtype=np.uint8)
+    signs = np.array([1, -1, -1, 1, -1], np.int8)
+    for slot0, L in ((0, 100), (16, 1024), (4096, 3000), (2**20 - 16, 80)):
+        acc = g.integers(0, 2**32, size=L, dtype=np.uint32)
+        want = acc.copy()
+        for s, sg in zip(seeds, signs):
+            p = O.prg(s.tobytes(), L, slot0)
+            want = want + p if sg == 1 else want - p
+        eng.mask_accumulate(seeds, signs, acc, slot0=slot0)
+        assert np.array_equal(acc, want), slot0
+
+
+def test_bad_arguments_raise(eng):
+    rows, seeds, signs = rand_case(1, 2, 2, 64)
+    with pytest.raises(RuntimeError):
+        eng.aggregate_unmask(list(rows), seeds, np.array([1, 0], np.int8))
+    with pytest.raises(RuntimeError):
+        eng.aggregate_unmask([rows[0], rows[1][:10]], seeds, signs)
+    with pytest.raises(RuntimeError):
+        eng.mask_accumulate(seeds, signs, np.zeros(32, np.uint32), slot0=8)
+
+
+# -------------------------------------------------------- device-resident
+def test_device_windows_sum_to_whole(eng):
+    """Slot-sharded unmask: per-shard windows reproduce the whole round."""
+    import torch
+    N, K, L = 96, 200, 3 * 4096 + 512
+    rows, seeds, signs = rand_case(77, N, K, L)
+    pitch = (L + 63) // 64 * 64
+    d_rows = torch.zeros((N, pitch), dtype=torch.int32, device="cuda")
+    d_rows[:, :L] = torch.from_numpy(rows.view(np.int32)).cuda()
+    d_seeds = torch.from_numpy(seeds).cuda()
+    d_signs = torch.from_numpy(signs).cuda()
+    want = O.aggregate_unmask(rows, seeds, signs, threads=8)
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    # G shards: rank g sums its client rows over all slots, masks only its slots
+    for G in (2, 3, 4):
+        bounds = [0] + [((L * (g + 1)) // G) // 16 * 16 for g in range(G - 1)] + [L]
+        parts = []
+        for g in range(G):
+            lo, hi = bounds[g], bounds[g + 1]
+            r0, r1 = N * g // G, N * (g + 1) // G
+            part = torch.empty(L, dtype=torch.int32, device="cuda")
+            eng.aggregate_unmask_dev(d_rows[r0:r1], d_seeds, d_signs, part, L=L, mask_lo=lo, mask_hi=hi)
+            parts.append(part)
+        torch.cuda.synchronize()
+        total = sum(p.cpu().numpy().view(np.uint32).astype(np.uint64) for p in parts) % 2**32
+        assert np.array_equal(total.astype(np.uint32), want), G
+    assert eng.check_signs() == 0
+
+
+@pytest.mark.parametrize("N,L", [(1024, 2**20), (4096, 2**18)])
+def test_full_size_invariant(eng, N, L):
+    """Benchmark-size round: valid masked rows made on the GPU, out == |U| everywhere."""
+    import torch
+    import flamingo_amd.params as P
+    g = rng(N + L)
+    m = g.integers(0, 256, size=(N, 32), dtype=np.uint8)
+    nbrs = P.synthetic_neighbors(N, degree=8, seed=N)
+    offline = np.sort(g.choice(N, max(1, N // 100), replace=False))
+    seg, cseeds, csigns = P.client_seed_table(m, nbrs, P.synthetic_pair_seed)
+    pitch = L
+    d_rows = torch.empty((N, pitch), dtype=torch.int32, device="cuda")
+    eng.client_mask_dev(seg, torch.from_numpy(cseeds).cuda(), csigns, d_rows, L)
+    online = np.setdiff1d(np.arange(N), offline)
+    sseeds, ssigns = P.server_seed_table(m, nbrs, online, offline, P.synthetic_pair_seed)
+    d_on = d_rows[torch.from_numpy(online).cuda()].contiguous()
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(d_on, torch.from_numpy(sseeds).cuda(), torch.from_numpy(ssigns).cuda(), out, L=L)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().view(np.uint32)
+    assert np.all(o == len(online)), np.flatnonzero(o != len(online))[:8]
+    # spot-check a slice of the masked rows against the oracle
+    i = int(online[3])
+    want = O.client_mask(seg[i:i + 2] - seg[i], cseeds[seg[i]:seg[i + 1]], csigns[seg[i]:seg[i + 1]], 4096)
+    assert np.array_equal(d_rows[i, :4096].cpu().numpy().view(np.uint32), want[0])
