@@ -110,8 +110,10 @@ def main():
     d_signs = torch.from_numpy(ssigns).to(dev)
     torch.cuda.synchronize()
 
+    # all round work (both launches and the reduce-scatter) on one dedicated stream
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     rnd = ShardedRound(eng, L)
-    stream = torch.cuda.current_stream()
 
     def step():
         rnd.prepare_seeds(d_seeds, d_signs, stream)

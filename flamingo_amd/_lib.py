@@ -40,6 +40,7 @@ SIGNATURES = {
     "flm_check_signs": (_int, [_vp, ctypes.POINTER(_int)]),
     "flm_last_plan": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
+    "flm_set_tuning": (_int, [_vp, ctypes.c_char_p, _int]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }
@@ -56,6 +57,13 @@ def load(path: str = LIB_PATH):
         raise RuntimeError(
             f"libflamingo_hip.so not found at {path}: build it with `python -m flamingo_amd.build` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Whichever loads first is used by both, and torch
+    # only initialises on its own, so let torch load it first when present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

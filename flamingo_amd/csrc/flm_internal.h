@@ -66,8 +66,15 @@ static_assert(sizeof(Item) == 64, "Item must be 64 bytes");
 // Launchers (flm_kernels.hip).  All enqueue on `stream` and return hipError_t.
 hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
                                 uint32_t *d_meta, hipStream_t stream);
+// items_kernel variants (see flm_kernels.hip): row load layout / accumulator form.
+enum ItemsVariant : int {
+    kVarCoalesced = 0,  // coalesced rows, separate row/mask accumulators (any plan)
+    kVarBlock = 1,      // block-layout rows, separate accumulators (any plan)
+    kVarMerged = 2,     // block-layout rows added into the mask accumulator (single-tile plans)
+    kVarMergedW8 = 3,   // kVarMerged at >= 8 waves/SIMD register budget
+};
 // subtiles: 1, 4 or 16 sub-tiles of 1024 slots per workgroup.
-hipError_t launch_items(int subtiles, const Item *d_items, int n_items, const uint32_t *d_rows,
+hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_items, const uint32_t *d_rows,
                         uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta,
                         uint32_t *d_out, hipStream_t stream);
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,

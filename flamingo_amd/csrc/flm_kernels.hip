@@ -40,30 +40,35 @@ namespace flm {
     c += d; b ^= c; b = FLM_ROTL(b, 7);
 
 // ------------------------------------------------------------------ seeds
-// Host-side twin of the first column round lives nowhere else: the schedule
-// is computed on the device from the raw seed bytes.
-__global__ __launch_bounds__(1024) void seed_schedule_kernel(const uint8_t *__restrict__ seeds,
-                                                             const int8_t *__restrict__ signs, int K,
-                                                             SeedRec *__restrict__ recs,
-                                                             uint32_t *__restrict__ meta) {
-    __shared__ uint32_t s_neg, s_bad;
-    if (threadIdx.x == 0) { s_neg = 0; s_bad = 0; }
-    __syncthreads();
+// One thread per seed builds its SeedRec from the raw 32 seed bytes and sign.
+// Workgroup p writes its count of negative / invalid signs to meta[2+2p],
+// meta[3+2p] and meta[0] = number of workgroups, so no zeroing pass is needed.
+__global__ __launch_bounds__(256) void seed_schedule_kernel(const uint8_t *__restrict__ seeds,
+                                                            const int8_t *__restrict__ signs, int K,
+                                                            SeedRec *__restrict__ recs,
+                                                            uint32_t *__restrict__ meta) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t neg = 0, bad = 0;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    if (k < K) {
         const uint8_t *p = seeds + 32 * (size_t)k;
         uint32_t key[8];
+        if (((uintptr_t)seeds & 15) == 0) {
+            const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
+            key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+            key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            key[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
-                     ((uint32_t)p[4 * i + 3] << 24);
-        const int s = signs[k];
-        neg += (s < 0);
-        bad += (s != 1 && s != -1);
+            for (int i = 0; i < 8; ++i)
+                key[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
+                         ((uint32_t)p[4 * i + 3] << 24);
+        }
+        const int sg = signs[k];
+        neg = (sg < 0);
+        bad = (sg != 1 && sg != -1);
         SeedRec r;
 #pragma unroll
         for (int i = 0; i < 8; ++i) r.k[i] = key[i];
-        r.xorc = s < 0 ? ~kAbcd : kAbcd;
+        r.xorc = sg < 0 ? ~kAbcd : kAbcd;
         r.a0 = kSigma0 + key[0];
         uint32_t x1 = kSigma1, x5 = key[1], x9 = key[5], x13 = 0u;
         uint32_t x2 = kSigma2, x6 = key[2], x10 = key[6], x14 = 0u;
@@ -81,10 +86,25 @@ __global__ __launch_bounds__(1024) void seed_schedule_kernel(const uint8_t *__re
         for (int i = 0; i < 7; ++i) r.pad[i] = 0;
         recs[k] = r;
     }
-    if (neg) atomicAdd(&s_neg, neg);
-    if (bad) atomicAdd(&s_bad, bad);
+    // workgroup totals (64-lane ballots, then 4 waves through LDS)
+    __shared__ uint32_t s_cnt[2][4];
+    const unsigned long long bn = __ballot(neg != 0), bb = __ballot(bad != 0);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_cnt[0][w] = __popcll(bn); s_cnt[1][w] = __popcll(bb); }
     __syncthreads();
-    if (threadIdx.x == 0) { meta[0] = s_neg; meta[1] = s_bad; }
+    if (threadIdx.x == 0) {
+        meta[2 + 2 * blockIdx.x] = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+        meta[3 + 2 * blockIdx.x] = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+        if (blockIdx.x == 0) meta[0] = gridDim.x;
+    }
+}
+
+// Total negative signs of the current seed table (sum of the per-workgroup counts).
+__device__ __forceinline__ uint32_t meta_nneg(const uint32_t *__restrict__ meta) {
+    const uint32_t parts = meta[0];
+    uint32_t n = 0;
+    for (uint32_t p = 0; p < parts; ++p) n += meta[2 + 2 * p];
+    return n;
 }
 
 // -------------------------------------------------------------- ChaCha core
@@ -158,12 +178,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Load the wave's 4 KiB of one row in coalesced layout through a buffer
 // descriptor whose range ends at the tile's last valid quad: quads past it
 // (tail tile) come back as zero from the hardware range check, no branches.
+// BL = block layout: lane t loads its own 64 B (slots 16t..16t+15), the layout
+// the ChaCha block is generated in; otherwise coalesced layout (slot 4t + 256j).
+template <bool BL>
 __device__ __forceinline__ void load_row(const uint32_t *base, uint32_t bytes, int lane, u32x4 (&v)[4]) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(base), 0,
                                                                         (int)bytes, 0x00020000);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        v[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane + 1024 * j, 0, 0));
+        v[j] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, BL ? 64 * lane + 16 * j : 16 * lane + 1024 * j, 0, 0));
 }
 
 // Sum the Cw chunk partials of every sub-tile from LDS and write the tile.
@@ -203,14 +227,22 @@ __device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32
 // --------------------------------------------------------------- main kernel
 // One workgroup = one Item.  Wave w works on sub-tile s = w % S with chunk
 // c = w / S of the item's rows and seeds (Cw = 16 / S chunks).
-template <int S>
-__global__ __launch_bounds__(kThreads) void items_kernel(const Item *__restrict__ items,
-                                                         const uint32_t *__restrict__ rows,
-                                                         uint64_t row_pitch,
-                                                         const SeedRec *__restrict__ recs,
-                                                         const uint32_t *__restrict__ meta,
-                                                         uint32_t *__restrict__ out) {
+//   BL      rows are loaded in block layout (lane t: slots 16t..16t+15), the
+//           layout the ChaCha blocks come out in; else coalesced layout.
+//   MERGED  every item writes one tile (same-tile, rows-only or mask-only), so
+//           rows are added straight into the mask accumulator (needs BL): one
+//           16-register accumulator instead of two, no transpose.
+//   WPE     minimum waves per SIMD requested from the register allocator.
+template <int S, bool BL, bool MERGED, int WPE>
+__global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__restrict__ items,
+                                                              const uint32_t *__restrict__ rows,
+                                                              uint64_t row_pitch,
+                                                              const SeedRec *__restrict__ recs,
+                                                              const uint32_t *__restrict__ meta,
+                                                              uint32_t *__restrict__ out) {
+    static_assert(!MERGED || BL, "merged accumulation needs block-layout rows");
     constexpr int Cw = kWavesPerGroup / S;
+    constexpr int RU = MERGED ? 2 : 4;  // rows in flight per wave in the rows-only loop
     __shared__ u32x4 lds[kWavesPerGroup * 256];  // 64 KiB: one 4 KiB region per wave
 
     const Item it = items[blockIdx.x];
@@ -220,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void items_kernel(const Item *__restrict_
     const uint32_t flags = it.flags;
     const bool has_rows = flags & kHasRows, has_mask = flags & kHasMask;
 
-    u32x4 racc[4] = {u32x4(0u), u32x4(0u), u32x4(0u), u32x4(0u)};
+    u32x4 racc[4] = {u32x4(0u), u32x4(0u), u32x4(0u), u32x4(0u)};  // unused when MERGED
     uint32_t m[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) m[i] = 0;
@@ -243,36 +275,44 @@ __global__ __launch_bounds__(kThreads) void items_kernel(const Item *__restrict_
     const uint32_t *rp = rows + it.row_in + (uint64_t)r0 * row_pitch + sub_slot;
     const uint32_t ctr = (uint32_t)(it.mask_ctr + (uint64_t)(sub_slot / 16) + (uint64_t)lane);
     const SeedRec *rec = recs + q0;
-
     if (row_valid <= 0) nr = 0;
+
+    auto add_row = [&](const u32x4 (&v)[4]) {
+        if constexpr (MERGED) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                m[4 * j + 0] += v[j].x; m[4 * j + 1] += v[j].y; m[4 * j + 2] += v[j].z; m[4 * j + 3] += v[j].w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[j];
+        }
+    };
+
     // paired phase: one row load in flight under one ChaCha block per step
     const uint32_t np = nr < ns ? nr : ns;
     for (uint32_t q = 0; q < np; ++q) {
         u32x4 v[4];
-        load_row(rp, row_bytes, lane, v);
+        load_row<BL>(rp, row_bytes, lane, v);
         chacha_mask_add(rec, ctr, m);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[j];
+        add_row(v);
         rp += row_pitch;
         ++rec;
     }
-    // remaining rows: four rows (16 KiB per wave) in flight
+    // remaining rows: RU rows (RU x 4 KiB per wave) in flight
     uint32_t rr = nr - np;
-    for (; rr >= 4; rr -= 4) {
-        u32x4 v[4][4];
+    for (; rr >= RU; rr -= RU) {
+        u32x4 v[RU][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) load_row(rp + u * row_pitch, row_bytes, lane, v[u]);
+        for (int u = 0; u < RU; ++u) load_row<BL>(rp + u * row_pitch, row_bytes, lane, v[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[u][j];
-        rp += 4 * row_pitch;
+        for (int u = 0; u < RU; ++u) add_row(v[u]);
+        rp += RU * row_pitch;
     }
     for (; rr > 0; --rr) {
         u32x4 v[4];
-        load_row(rp, row_bytes, lane, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) racc[j] = racc[j] + v[j];
+        load_row<BL>(rp, row_bytes, lane, v);
+        add_row(v);
         rp += row_pitch;
     }
     // remaining seeds
@@ -281,41 +321,63 @@ __global__ __launch_bounds__(kThreads) void items_kernel(const Item *__restrict_
         ++rec;
     }
 
-    // ---- combine: block layout -> coalesced layout through this wave's LDS region
+    // ---- combine through this wave's LDS region (natural slot order), then
+    // sum the Cw chunk partials of every sub-tile and write the tile.
     u32x4 *R = lds + w * 256;
-    const bool same = flags & kSameTile;
-    u32x4 mq[4];
-    if (has_mask) {
+    const uint32_t mbias = it.mask_bias + ((flags & kMaskBiasNneg) ? meta_nneg(meta) : 0u);
+    if constexpr (MERGED) {
         R[4 * lane + 0] = u32x4{m[0], m[1], m[2], m[3]};
         R[4 * lane + 1] = u32x4{m[4], m[5], m[6], m[7]};
         R[4 * lane + 2] = u32x4{m[8], m[9], m[10], m[11]};
         R[4 * lane + 3] = u32x4{m[12], m[13], m[14], m[15]};
         __syncthreads();
+        const uint64_t base = has_mask ? it.mask_out : it.row_out;
+        const int valid = has_mask ? (int)it.mask_valid : (int)it.row_valid;
+        const uint32_t bias = (has_rows ? it.row_bias : 0u) + (has_mask ? mbias : 0u);
+        reduce_out<S>(lds, out, base, valid, bias, (flags & (kRowAtomic | kMaskAtomic)) != 0);
+    } else {
+        const bool same = flags & kSameTile;
+        u32x4 mq[4];
+        if (has_mask) {
+            if (BL) {
+                mq[0] = u32x4{m[0], m[1], m[2], m[3]};
+                mq[1] = u32x4{m[4], m[5], m[6], m[7]};
+                mq[2] = u32x4{m[8], m[9], m[10], m[11]};
+                mq[3] = u32x4{m[12], m[13], m[14], m[15]};
+            } else {  // block layout -> coalesced layout
+                R[4 * lane + 0] = u32x4{m[0], m[1], m[2], m[3]};
+                R[4 * lane + 1] = u32x4{m[4], m[5], m[6], m[7]};
+                R[4 * lane + 2] = u32x4{m[8], m[9], m[10], m[11]};
+                R[4 * lane + 3] = u32x4{m[12], m[13], m[14], m[15]};
+                __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mq[j] = R[lane + 64 * j];
-        if (same) {
+                for (int j = 0; j < 4; ++j) mq[j] = R[lane + 64 * j];
+            }
+            if (same) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) racc[j] = racc[j] + mq[j];
+                for (int j = 0; j < 4; ++j) racc[j] = racc[j] + mq[j];
+            }
         }
-    }
-    const uint32_t nneg = meta[0];
-    const uint32_t mbias = it.mask_bias + ((flags & kMaskBiasNneg) ? nneg : 0u);
-    if (has_rows || same) {
+        // LDS quad index of accumulator quad j of this lane (natural slot order)
+#define FLM_RQ(j) (BL ? 4 * lane + (j) : lane + 64 * (j))
+        if (has_rows || same) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) R[lane + 64 * j] = racc[j];
-        __syncthreads();
-        const uint64_t base = same ? it.mask_out : it.row_out;
-        const int valid = same ? (int)it.mask_valid : (int)it.row_valid;
-        const uint32_t bias = it.row_bias + (same ? mbias : 0u);
-        const bool atom = same ? ((flags & (kRowAtomic | kMaskAtomic)) != 0) : ((flags & kRowAtomic) != 0);
-        reduce_out<S>(lds, out, base, valid, bias, atom);
-    }
-    if (has_mask && !same) {
-        __syncthreads();
+            for (int j = 0; j < 4; ++j) R[FLM_RQ(j)] = racc[j];
+            __syncthreads();
+            const uint64_t base = same ? it.mask_out : it.row_out;
+            const int valid = same ? (int)it.mask_valid : (int)it.row_valid;
+            const uint32_t bias = it.row_bias + (same ? mbias : 0u);
+            const bool atom = same ? ((flags & (kRowAtomic | kMaskAtomic)) != 0) : ((flags & kRowAtomic) != 0);
+            reduce_out<S>(lds, out, base, valid, bias, atom);
+        }
+        if (has_mask && !same) {
+            __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; ++j) R[lane + 64 * j] = mq[j];
-        __syncthreads();
-        reduce_out<S>(lds, out, it.mask_out, (int)it.mask_valid, mbias, (flags & kMaskAtomic) != 0);
+            for (int j = 0; j < 4; ++j) R[FLM_RQ(j)] = mq[j];
+            __syncthreads();
+            reduce_out<S>(lds, out, it.mask_out, (int)it.mask_valid, mbias, (flags & kMaskAtomic) != 0);
+        }
+#undef FLM_RQ
     }
 }
 
@@ -359,31 +421,39 @@ __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t
 // ----------------------------------------------------------------- launchers
 hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
                                 uint32_t *d_meta, hipStream_t stream) {
-    hipLaunchKernelGGL(seed_schedule_kernel, dim3(1), dim3(1024), 0, stream, d_seeds, d_signs, K, d_recs,
-                       d_meta);
+    const unsigned grid = (unsigned)((K + 255) / 256 > 0 ? (K + 255) / 256 : 1);
+    hipLaunchKernelGGL(seed_schedule_kernel, dim3(grid), dim3(256), 0, stream, d_seeds, d_signs, K, d_recs, d_meta);
     return hipGetLastError();
 }
 
-hipError_t launch_items(int subtiles, const Item *d_items, int n_items, const uint32_t *d_rows,
-                        uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta,
-                        uint32_t *d_out, hipStream_t stream) {
+template <int S, bool BL, bool MERGED, int WPE>
+static void launch_items_t(const Item *d_items, int n_items, const uint32_t *d_rows, uint64_t row_pitch,
+                           const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out, hipStream_t stream) {
+    hipLaunchKernelGGL((items_kernel<S, BL, MERGED, WPE>), dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+                       row_pitch, d_recs, d_meta, d_out);
+}
+
+hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_items, const uint32_t *d_rows,
+                        uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out,
+                        hipStream_t stream) {
     if (n_items <= 0) return hipSuccess;
-    switch (subtiles) {
-        case 1:
-            hipLaunchKernelGGL(items_kernel<1>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
-                               row_pitch, d_recs, d_meta, d_out);
-            break;
-        case 4:
-            hipLaunchKernelGGL(items_kernel<4>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
-                               row_pitch, d_recs, d_meta, d_out);
-            break;
-        case 16:
-            hipLaunchKernelGGL(items_kernel<16>, dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
-                               row_pitch, d_recs, d_meta, d_out);
-            break;
-        default:
-            return hipErrorInvalidValue;
+#define FLM_L(S, BL, MG, W) launch_items_t<S, BL, MG, W>(d_items, n_items, d_rows, row_pitch, d_recs, d_meta, d_out, stream)
+#define FLM_V(S)                                                     \
+    switch (variant) {                                               \
+        case kVarCoalesced: FLM_L(S, false, false, 4); break;        \
+        case kVarBlock: FLM_L(S, true, false, 4); break;             \
+        case kVarMerged: FLM_L(S, true, true, 4); break;             \
+        case kVarMergedW8: FLM_L(S, true, true, 8); break;           \
+        default: return hipErrorInvalidValue;                        \
     }
+    switch (subtiles) {
+        case 1: FLM_V(1) break;
+        case 4: FLM_V(4) break;
+        case 16: FLM_V(16) break;
+        default: return hipErrorInvalidValue;
+    }
+#undef FLM_V
+#undef FLM_L
     return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -66,6 +67,7 @@ struct Plan {
     int subtiles = 1;
     bool needs_zero = false;
     int atomics = 0;
+    bool single_tile = true;  // every item writes one tile (merged accumulator legal)
 };
 
 using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>;
@@ -81,6 +83,8 @@ struct flm_ctx {
     Plan scratch_plan;  // uncached plans (client masking, expansion)
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
     int table_k = -1;  // seeds in the current device seed table
+    int tune_variant = -1;   // items_kernel variant, -1 = auto
+    int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
 };
 
 namespace {
@@ -118,7 +122,7 @@ struct Unit {
 };
 
 void plan_job(const Job &j, uint64_t pitch, int subtiles, int parts_r, int parts_m, std::vector<Item> &items,
-              bool &needs_zero, int &atomics) {
+              bool &needs_zero, int &atomics, bool &single_tile) {
     const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
     std::vector<Unit> R, M;
     if (j.nrows > 0 && j.L > 0) {
@@ -147,6 +151,7 @@ void plan_job(const Job &j, uint64_t pitch, int subtiles, int parts_r, int parts
     if (atomic) needs_zero = true;
     if (R.empty() && (j.mask_lo > 0 || j.mask_hi < j.L || M.empty())) needs_zero = true;
     atomics |= atomic ? 1 : 0;
+    if (both && !paired_same) single_tile = false;
 
     const size_t n = std::max(R.size(), M.size());
     for (size_t i = 0; i < n; ++i) {
@@ -197,6 +202,15 @@ int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t ns
     return 0;
 }
 
+int pick_variant(const flm_ctx *ctx, const Plan &plan) {
+    int v = ctx->tune_variant;
+    // measured (tools/ab_items.py, profiles/r01_ab_items.log): merged accumulator
+    // fastest where legal, block-layout rows next
+    if (v < 0) v = plan.single_tile ? flm::kVarMerged : flm::kVarBlock;
+    if (!plan.single_tile && (v == flm::kVarMerged || v == flm::kVarMergedW8)) v = flm::kVarBlock;
+    return v;
+}
+
 int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
     plan.n_items = (int)items.size();
     if (items.empty()) return 0;
@@ -207,10 +221,14 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
 
 Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
                      uint64_t prg_slot0, int *rc) {
-    PlanKey key{0, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
+    // ChaCha-heavy rounds keep 1024-slot tiles (16 waves split one tile's seeds);
+    // row-streaming-heavy rounds (few seeds per slot) prefer 4 sub-tiles per
+    // workgroup: 4096-slot tiles, fewer LDS combines (measured 5.77 vs 5.26 TB/s).
+    const bool seed_light = (uint64_t)K * (mask_hi - mask_lo) * 2 < (uint64_t)N * L;
+    const int subtiles = ctx->tune_subtiles > 0 ? ctx->tune_subtiles : (seed_light ? 4 : 1);
+    PlanKey key{subtiles, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
     auto f = ctx->plans.find(key);
     if (f != ctx->plans.end()) { *rc = 0; return f->second; }
-    const int subtiles = 1;
     const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
     Job j;
     j.nrows = (uint32_t)N;
@@ -227,7 +245,7 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
     std::vector<Item> items;
     Plan *plan = new Plan();
     plan->subtiles = subtiles;
-    plan_job(j, pitch, subtiles, pr, pm, items, plan->needs_zero, plan->atomics);
+    plan_job(j, pitch, subtiles, pr, pm, items, plan->needs_zero, plan->atomics, plan->single_tile);
     *rc = upload_plan(ctx, *plan, items);
     if (*rc) { plan->items.release(); delete plan; return nullptr; }
     if (ctx->plans.size() > 64) {  // bound the cache
@@ -257,21 +275,22 @@ int check_range(flm_ctx *ctx, uint64_t slot_hi) {
 
 int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s) {
     FLM_HIP(ctx, ctx->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec)));
-    FLM_HIP(ctx, ctx->meta.reserve(64));
+    FLM_HIP(ctx, ctx->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)((std::max(K, 1) + 255) / 256))));
     FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s));
     ctx->table_k = K;
     return 0;
 }
 
 int run_plan(flm_ctx *ctx, const Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
-             size_t out_elems, hipStream_t s, int variant) {
+             size_t out_elems, hipStream_t s) {
     if (plan.needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
-    FLM_HIP(ctx, flm::launch_items(plan.subtiles, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
+    const int variant_id = pick_variant(ctx, plan);
+    FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
                                    ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * plan.subtiles;
     ctx->last_atomics = plan.atomics;
-    ctx->last_variant = variant;
+    ctx->last_variant = variant_id;
     return 0;
 }
 
@@ -300,10 +319,10 @@ int upload_seeds(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K)
 // workgroup (each wave its own 1024 slots, all of the row's seeds).
 // out[i] = (x[i] or base_bias) + sum of row i's seeds (+1 per negative seed).
 int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, const int64_t *seg, const int8_t *signs,
-                  uint32_t base_bias, size_t L, uint64_t slot0, uint32_t *d_out, hipStream_t s, int variant) {
+                  uint32_t base_bias, size_t L, uint64_t slot0, uint32_t *d_out, hipStream_t s) {
     const int subtiles = 16;
     std::vector<Item> items;
-    bool needs_zero = false;
+    bool needs_zero = false, single_tile = true;
     int atomics = 0;
     for (int i = 0; i < N; ++i) {
         Job j;
@@ -341,20 +360,22 @@ int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, cons
         j.mask_hi = L;
         j.prg_slot0 = slot0;
         j.mask_bias = bias;
-        plan_job(j, pitch, subtiles, 1, 1, items, needs_zero, atomics);
+        plan_job(j, pitch, subtiles, 1, 1, items, needs_zero, atomics, single_tile);
     }
     Plan &plan = ctx->scratch_plan;
     plan.subtiles = subtiles;
     plan.needs_zero = needs_zero;
     plan.atomics = atomics;
+    plan.single_tile = single_tile;
     if (int rc = upload_plan(ctx, plan, items)) return rc;
     if (needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)N * pitch * sizeof(uint32_t), s));
-    FLM_HIP(ctx, flm::launch_items(subtiles, plan.items.as<Item>(), plan.n_items, d_x, pitch, ctx->recs.as<SeedRec>(),
+    const int variant_id = pick_variant(ctx, plan);
+    FLM_HIP(ctx, flm::launch_items(subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_x, pitch, ctx->recs.as<SeedRec>(),
                                    ctx->meta.as<uint32_t>(), d_out, s));
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * subtiles;
     ctx->last_atomics = atomics;
-    ctx->last_variant = variant;
+    ctx->last_variant = variant_id;
     return 0;
 }
 
@@ -443,7 +464,8 @@ static int check_aggregate_args(flm_ctx *ctx, const uint32_t *d_rows, size_t row
         return fail(ctx, FLM_EINVAL, "rows and out must be 16-byte aligned");
     if (mask_hi > L || mask_lo > mask_hi)
         return fail(ctx, FLM_EINVAL, "mask window [%zu,%zu) outside [0,%zu)", mask_lo, mask_hi, L);
-    if (mask_lo % 16 || prg_slot0 % 16) return fail(ctx, FLM_EINVAL, "mask_lo and prg_slot0 must be multiples of 16");
+    if ((mask_hi > mask_lo && mask_lo % 16) || prg_slot0 % 16)
+        return fail(ctx, FLM_EINVAL, "mask_lo and prg_slot0 must be multiples of 16");
     if (int rc = check_range(ctx, prg_slot0 + mask_hi)) return rc;
     if (N > 0 && !d_rows) return fail(ctx, FLM_EINVAL, "rows is NULL");
     if (!d_out) return fail(ctx, FLM_EINVAL, "out is NULL");
@@ -454,7 +476,7 @@ int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     return run_seed_schedule(ctx, d_seeds, d_signs, K, s);
 }
@@ -465,12 +487,12 @@ int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, in
     if (L == 0) return 0;
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
     if (K != ctx->table_k) return fail(ctx, FLM_EINVAL, "K=%d does not match the seed table (%d)", K, ctx->table_k);
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     int rc = 0;
     Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
     if (!plan) return rc;
-    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s, 1);
+    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s);
 }
 
 int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
@@ -528,13 +550,13 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     if (K > 0 && (!d_seeds || !signs)) return fail(ctx, FLM_EINVAL, "NULL seeds/signs");
     if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     // signs go to the device with the seeds (the schedule folds them into xorc)
     FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
     if (K > 0) FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, s));
     if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), (int)K, s)) return rc;
-    return run_rows_jobs(ctx, d_x, pitch, N, seg, signs, 1u, L, 0, d_out, s, 2);
+    return run_rows_jobs(ctx, d_x, pitch, N, seg, signs, 1u, L, 0, d_out, s);
 }
 
 int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t slot0, uint32_t *out) {
@@ -566,7 +588,7 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     if (pitch % 4 || pitch < round_up(L, 4)) return fail(ctx, FLM_EINVAL, "pitch must be a multiple of 4 and >= L");
     if ((uintptr_t)d_out & 15) return fail(ctx, FLM_EINVAL, "out must be 16-byte aligned");
     if (int rc = check_range(ctx, slot0 + L)) return rc;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     std::vector<int8_t> plus((size_t)K, 1);
     FLM_HIP(ctx, ctx->signs.reserve((size_t)K));
@@ -574,7 +596,7 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), K, s)) return rc;
     // the staging vector must outlive the async copy
     FLM_HIP(ctx, hipStreamSynchronize(s));
-    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, 0u, L, slot0, d_out, s, 3);
+    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, 0u, L, slot0, d_out, s);
 }
 
 int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *acc, size_t L,
@@ -624,12 +646,31 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
     return 0;
 }
 
+int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
+    if (!ctx || !key) return fail(ctx, FLM_EINVAL, "NULL argument");
+    const std::string k(key);
+    if (k == "variant") {
+        if (value < -1 || value > flm::kVarMergedW8) return fail(ctx, FLM_EINVAL, "variant %d out of range", value);
+        ctx->tune_variant = value;
+    } else if (k == "subtiles") {
+        if (value != 0 && value != 1 && value != 4 && value != 16)
+            return fail(ctx, FLM_EINVAL, "subtiles must be 0 (auto), 1, 4 or 16");
+        ctx->tune_subtiles = value;
+    } else {
+        return fail(ctx, FLM_EINVAL, "unknown tuning key '%s'", key);
+    }
+    return 0;
+}
+
 int flm_check_signs(flm_ctx *ctx, int *bad_count) {
     if (!ctx || !bad_count) return fail(ctx, FLM_EINVAL, "NULL argument");
-    uint32_t meta[2] = {0, 0};
-    if (!ctx->meta.p) { *bad_count = 0; return 0; }
-    FLM_HIP(ctx, hipMemcpy(meta, ctx->meta.p, sizeof meta, hipMemcpyDeviceToHost));
-    *bad_count = (int)meta[1];
+    *bad_count = 0;
+    if (!ctx->meta.p) return 0;
+    uint32_t parts = 0;
+    FLM_HIP(ctx, hipMemcpy(&parts, ctx->meta.p, sizeof parts, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> m(2 + 2 * (size_t)parts);
+    FLM_HIP(ctx, hipMemcpy(m.data(), ctx->meta.p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t p = 0; p < parts; ++p) *bad_count += (int)m[3 + 2 * p];
     return 0;
 }
 

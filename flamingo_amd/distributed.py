@@ -45,7 +45,7 @@ def client_bounds(N: int, world: int, rank: int):
 class ShardedRound:
     """Runs one rank's share of a round on its GPU and reduce-scatters the partials."""
 
-    def __init__(self, engine, L: int, group=None):
+    def __init__(self, engine, L: int, group=None, device=None):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -53,7 +53,7 @@ class ShardedRound:
         self.L = L
         self.Lp = padded_length(L, self.world)
         self.lo, self.hi = shard_bounds(L, self.world, self.rank)
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.partial = torch.zeros(self.Lp, dtype=torch.int32, device=dev)
         self.out = torch.empty(self.Lp // self.world, dtype=torch.int32, device=dev)
 

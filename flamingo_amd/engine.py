@@ -85,6 +85,10 @@ class MaskEngine:
         if rc != 0:
             raise RuntimeError(f"{what}: {self.lib.flm_last_error(self.ctx).decode()} (code {rc})")
 
+    def set_tuning(self, key: str, value: int):
+        """A/B knobs: variant (-1 auto, 0..3) and subtiles (0 auto, 1, 4, 16)."""
+        self._check(self.lib.flm_set_tuning(self.ctx, key.encode(), int(value)), f"flm_set_tuning({key})")
+
     def last_plan(self) -> dict:
         v = [ctypes.c_int() for _ in range(4)]
         self.lib.flm_last_plan(self.ctx, *[ctypes.byref(x) for x in v])

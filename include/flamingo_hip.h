@@ -23,7 +23,7 @@
  *  - Host-pointer functions are synchronous: they copy in, compute on the
  *    GPU and copy out; no host pointer is retained after return.
  *  - *_dev functions take device pointers and enqueue work on `stream`
- *    (a hipStream_t; NULL = the context's own stream) without synchronising.
+ *    (a hipStream_t; NULL = the HIP null stream) without synchronising.
  *  - One context per host thread; a context binds one GPU (one process per
  *    GPU).  Create it lazily, after any fork (SA_ServiceAgent.py:562 forks a
  *    multiprocessing.Pool).
@@ -137,6 +137,14 @@ int flm_check_signs(flm_ctx *ctx, int *bad_count);
 /* Describe the launch plan the last *aggregate* call used:
  * items, tile slots, atomics used (0/1), kernel variant id. */
 int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics, int *variant);
+
+/* Tuning knobs for A/B measurement (defaults are the tuned choice):
+ *   "variant"  -1 auto | 0 coalesced rows | 1 block-layout rows |
+ *              2 merged accumulator | 3 merged, 8 waves/SIMD budget
+ *              (2/3 apply only to plans whose items each write one tile)
+ *   "subtiles" 0 auto | 1 | 4 | 16 sub-tiles of 1024 slots per workgroup
+ *              for aggregate plans. */
+int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */

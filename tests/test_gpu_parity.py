@@ -225,3 +225,44 @@ def test_full_size_invariant(eng, N, L):
     i = int(online[3])
     want = O.client_mask(seg[i:i + 2] - seg[i], cseeds[seg[i]:seg[i + 1]], csigns[seg[i]:seg[i + 1]], 4096)
     assert np.array_equal(d_rows[i, :4096].cpu().numpy().view(np.uint32), want[0])
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("subtiles", [0, 1, 4, 16])
+def test_kernel_variants_bit_identical(eng, variant, subtiles):
+    """Every items_kernel variant / tiling gives the oracle's bits (incl. tails, K > 256)."""
+    eng.set_tuning("variant", variant)
+    eng.set_tuning("subtiles", subtiles)
+    try:
+        for N, K, L in ((40, 300, 5000), (3, 700, 16000), (64, 5, 70000)):
+            rows, seeds, signs = rand_case(N + K + L + subtiles, N, K, L)
+            want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+            assert np.array_equal(eng.aggregate_unmask(list(rows), seeds, signs, L=L), want), (N, K, L)
+    finally:
+        eng.set_tuning("variant", -1)
+        eng.set_tuning("subtiles", 0)
+
+
+def test_sharded_windows_variants(eng):
+    """Dual-tile plans (rows and masks on different tiles) for each variant."""
+    import torch
+    N, K, L = 50, 90, 9000
+    rows, seeds, signs = rand_case(5, N, K, L)
+    d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+    d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+    want_rows = O.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8))
+    lo, hi = 2048, 6144
+    want = want_rows.copy()
+    want[lo:hi] += O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds, signs, L=hi - lo, slot0=lo)
+    for v in (-1, 0, 1, 2):
+        eng.set_tuning("variant", v)
+        out = torch.empty(L, dtype=torch.int32, device="cuda")
+        eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), v
+    eng.set_tuning("variant", -1)
+    # empty shard (rank owning no slots) with an unaligned clipped bound
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=L, mask_hi=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want_rows)

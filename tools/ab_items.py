@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""A/B the items_kernel variants in one process (interleaved rounds, same device).
+
+Workloads (all N=1024 rows x L=2^20 slots, device resident, random rows):
+  full     K=1024 self-mask seeds over all slots (G=1 round)
+  pairs    K=204 dropout-pair seeds (HBM-bound half)
+  shard8   K=8192 seeds over a 1/8 slot window (one rank of the 8-GPU weak-scaled round)
+Prints median/min kernel ms and GB/s per (workload, variant, subtiles), and
+checks every variant returns identical bits.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flamingo_amd import MaskEngine  # noqa: E402
+
+VARIANTS = {"coalesced": 0, "block": 1, "merged": 2, "merged_w8": 3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--workloads", default="full,pairs,shard8")
+    ap.add_argument("--variants", default="coalesced,block,merged,merged_w8")
+    ap.add_argument("--subtiles", default="1,4")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    eng = MaskEngine(0)
+    N, L = 1024, 1 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    rows = torch.randint(-2**31, 2**31 - 1, (N, L), dtype=torch.int32, device="cuda", generator=g)
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    res = []
+    for wl in args.workloads.split(","):
+        K = {"full": 1024, "pairs": 204, "shard8": 8192}[wl]
+        lo, hi = (0, L) if wl != "shard8" else (3 * L // 8, 4 * L // 8)
+        seeds = torch.randint(0, 256, (K, 32), dtype=torch.uint8, device="cuda", generator=g)
+        signs = (torch.randint(0, 2, (K,), device="cuda", generator=g) * 2 - 1).to(torch.int8)
+        eng.seed_table_dev(seeds, signs, stream=s)
+        times = {}
+        ref = None
+        combos = [(v, st) for v in args.variants.split(",") for st in map(int, args.subtiles.split(","))]
+        for rnd in range(args.rounds):
+            for v, st in combos:
+                eng.set_tuning("variant", VARIANTS[v])
+                eng.set_tuning("subtiles", st)
+                eng.aggregate_dev(rows, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=s)  # warm / plan
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
+                e[0].record(s)
+                for r in range(args.reps):
+                    eng.aggregate_dev(rows, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=s)
+                    e[r + 1].record(s)
+                torch.cuda.synchronize()
+                ms = [e[i].elapsed_time(e[i + 1]) for i in range(args.reps)]
+                times.setdefault((v, st), []).extend(ms)
+                o = out.cpu().numpy()
+                if ref is None:
+                    ref = o.copy()
+                elif not np.array_equal(ref, o):
+                    print(f"MISMATCH {wl} {v} st={st}", flush=True)
+                plan = eng.last_plan()
+        for (v, st), ms in times.items():
+            med, mn = float(np.median(ms)), float(np.min(ms))
+            gbs = (4.0 * N * L + 4.0 * L) / (med * 1e-3) / 1e9
+            r = {"workload": wl, "variant": v, "subtiles": st, "median_ms": round(med, 4), "min_ms": round(mn, 4),
+                 "GB/s": round(gbs, 1)}
+            res.append(r)
+            print(json.dumps(r), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
