@@ -1,0 +1,113 @@
+"""Flamingo experiment driver (config/flamingo.py surface).
+
+    python -m flamingo_amd.abides -c flamingo -n 128 -i 1 [-o 1] [-s SEED] [-v]
+
+Same flags as the reference (config/flamingo.py:24-52), same agent
+construction (:179-215), cubic latency model (:225-238) and result print
+(:253-266).  Extra flags: --vector_len (reference constant 16000,
+util/param.py:8), --root_seed_hex (the reference draws it at random,
+util/param.py:31), --offline id,id,... (clients that crash before sending in
+every iteration: explicit dropout injection).
+"""
+from __future__ import annotations
+
+import argparse
+from datetime import timedelta
+from time import time
+
+import numpy as np
+import pandas as pd
+
+from . import log
+from .kernel import Kernel
+from .latency import LatencyModel
+from .flamingo import SA_ClientAgent as ClientAgent
+from .flamingo import SA_ServiceAgent as ServiceAgent
+from .flamingo import protocol as param
+from .. import params as P
+
+
+def parse(argv):
+    ap = argparse.ArgumentParser(description="Detailed options for the Flamingo config.")
+    ap.add_argument("-a", "--clear_learning", action="store_true")
+    ap.add_argument("-c", "--config", required=True)
+    ap.add_argument("-i", "--num_iterations", type=int, default=5)
+    ap.add_argument("-k", "--skip_log", action="store_true")
+    ap.add_argument("-l", "--log_dir", default=None)
+    ap.add_argument("-n", "--num_clients", type=int, default=5)
+    ap.add_argument("-o", "--neighborhood_size", type=int, default=1)
+    ap.add_argument("--round_time", type=int, default=10)
+    ap.add_argument("-s", "--seed", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("-p", "--parallel_mode", type=bool, default=True)   # type=bool quirk kept
+    ap.add_argument("-d", "--debug_mode", type=bool, default=False)
+    ap.add_argument("--config_help", action="store_true")
+    ap.add_argument("--vector_len", type=int, default=P.vector_len)
+    ap.add_argument("--root_seed_hex", default=None)
+    ap.add_argument("--offline", default="")
+    args, _ = ap.parse_known_args(argv)
+    return ap, args
+
+
+def run(argv=None):
+    ap, args = parse(argv)
+    if args.config_help:
+        ap.print_help()
+        return None
+    seed = args.seed or int(pd.Timestamp.now().timestamp() * 1000000) % (2**32 - 1)
+    np.random.seed(seed)
+    log.silent_mode = not args.verbose
+    n = args.num_clients
+    if not P.assert_power_of_two(n):
+        raise ValueError("Number of clients must be power of 2")
+    root = bytes.fromhex(args.root_seed_hex) if args.root_seed_hex else None
+    param.configure(root=root, L=args.vector_len)
+    offline = {int(x) for x in args.offline.split(",") if x.strip()}
+    print(f"Silent mode: {log.silent_mode}")
+    print(f"Configuration seed: {seed}\n")
+
+    start = pd.to_datetime("2023-01-01")
+    stop = start + pd.to_timedelta("2000:00:00")
+    default_delay = 1000000000 * 0.1
+    kernel = Kernel("Base Kernel",
+                    random_state=np.random.RandomState(seed=np.random.randint(low=0, high=2**32, dtype="uint64")))
+    latency_rstate = np.random.RandomState(seed=np.random.randint(low=0, high=2**32, dtype="uint64"))
+    agents = []
+    t0 = time()
+    for i in range(n):
+        agents.append(ClientAgent(
+            id=i, name=f"PPFL Client Agent {i}", type="ClientAgent", iterations=args.num_iterations, num_clients=n,
+            neighborhood_size=args.neighborhood_size, debug_mode=args.debug_mode,
+            random_state=np.random.RandomState(seed=np.random.randint(low=0, high=2**32, dtype="uint64")),
+            offline_iterations=range(1, args.num_iterations + 1) if i in offline else ()))
+    print(f"Client init took {timedelta(seconds=time() - t0)}")
+    server = ServiceAgent(
+        id=n, name="PPFL Service Agent", type="ServiceAgent",
+        random_state=np.random.RandomState(seed=np.random.randint(low=0, high=2**32, dtype="uint64")),
+        msg_fwd_delay=0, users=[*range(n)], iterations=args.num_iterations,
+        round_time=pd.Timedelta(f"{args.round_time}s"), num_clients=n, neighborhood_size=args.neighborhood_size,
+        parallel_mode=args.parallel_mode, debug_mode=args.debug_mode)
+    agents.append(server)
+    pairwise = (len(agents), len(agents))
+    model_args = {"connected": True,
+                  "min_latency": np.random.uniform(low=10000000, high=100000000, size=pairwise),
+                  "jitter": 0.3, "jitter_clip": 0.05, "jitter_unit": 5}
+    latency = LatencyModel(latency_model="cubic", random_state=latency_rstate, kwargs=model_args)
+    results = kernel.runner(agents=agents, startTime=start, stopTime=stop, agentLatencyModel=latency,
+                            defaultComputationDelay=default_delay, skip_log=args.skip_log, log_dir=args.log_dir)
+    print()
+    print("######## Microbenchmarks ########")
+    print(f"Protocol Iterations: {args.num_iterations}, Clients: {n}, ")
+    print()
+    print("Service Agent mean time per iteration (except setup)...")
+    print(f"    Report step:         {results['srv_report']}")
+    print(f"    Crosscheck step:     {results['srv_crosscheck']}")
+    print(f"    Reconstruction step: {results['srv_reconstruction']}")
+    print()
+    print("Client Agent mean time per iteration (except setup)...")
+    print(f"    Report step:         {results['clt_report'] / n}")
+    print(f"    Crosscheck step:     {results['clt_crosscheck'] / param.committee_size}")
+    print(f"    Reconstruction step: {results['clt_reconstruction'] / param.committee_size}")
+    print()
+    results["server"] = server
+    return results

@@ -1,0 +1,253 @@
+"""Flamingo server agent (agent/flamingo/SA_ServiceAgent.py surface).
+
+Four-step round state machine, same as the reference (:123-135):
+  0 initialize          choose committee, deal the decryption-key shares
+  1 report              collect VECTORs; partial sum S; dropout pairs + signs
+  2 forward_signatures  forward the committee's signed offline set (DEC)
+  3 reconstruction      recover m_i from committee shares; unmask; combine
+
+The hot loops are replaced by calls into the MI355X engine:
+  report_process        S = sum_{i in U} y_i         (:346-350)  -> MaskEngine.aggregate_unmask(rows, K=0)
+  reconstruction_process out = S - sum PRG(m_i) + sum sigma PRG(s_ij)
+                        (:529-540, :587-605)          -> MaskEngine.mask_accumulate(seeds, signs, S)
+Both are bit-exact with the reference's numpy uint32 arithmetic.  Seed
+transport (Shamir real, encryption stand-in) is described in seeds.py.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import logging
+
+import numpy as np
+import pandas as pd
+
+from ..agent import Agent
+from ..message import Message
+from . import protocol as param
+from .seeds import P256_N, lagrange_at_zero, shamir_share
+from ... import params as P
+
+
+class SA_ServiceAgent(Agent):
+    def __str__(self):
+        return "[server]"
+
+    def __init__(self, id, name, type, random_state=None, msg_fwd_delay=1000000, round_time=pd.Timedelta("10s"),
+                 iterations=4, key_length=32, num_clients=10, neighborhood_size=1, parallel_mode=1, debug_mode=0,
+                 users={}):
+        super().__init__(id, name, type, random_state)
+        self.logger = logging.getLogger(__name__)
+        self.logger.setLevel(logging.INFO)
+        if debug_mode:
+            logging.basicConfig()
+        self.msg_fwd_delay = msg_fwd_delay
+        self.round_time = round_time
+        self.no_of_iterations = iterations
+        self.parallel_mode = parallel_mode
+        self.num_clients = num_clients
+        self.users = users
+        self.vector_len = param.vector_len
+        self.vector_dtype = param.vector_type
+        self.vec_sum_partial = np.zeros(self.vector_len, dtype=self.vector_dtype)
+        self.final_sum = np.zeros(self.vector_len, dtype=self.vector_dtype)
+        self.prime = P256_N
+        self.key_length = key_length
+        self.neighborhood_size = neighborhood_size
+        self.committee_threshold = 0
+        self.elapsed_time = {"REPORT": pd.Timedelta(0), "CROSSCHECK": pd.Timedelta(0),
+                             "RECONSTRUCTION": pd.Timedelta(0)}
+        self.user_vectors, self.pairwise_cipher, self.mi_cipher, self.recon_index = {}, {}, {}, {}
+        self.recv_user_vectors, self.recv_pairwise_cipher, self.recv_mi_cipher, self.recv_recon_index = {}, {}, {}, {}
+        self.user_committee = set()
+        self.committee_shares_pairwise, self.committee_shares_mi, self.committee_sigs = {}, {}, {}
+        self.recv_committee_shares_pairwise, self.recv_committee_shares_mi, self.recv_committee_sigs = {}, {}, {}
+        self.dec_target_pairwise, self.recon_symbol = {}, {}
+        self.current_iteration = 1
+        self.current_round = 0
+        self.results = {}            # iteration -> final_sum (kept for inspection / tests)
+        self.aggProcessingMap = {0: self.initialize, 1: self.report, 2: self.forward_signatures,
+                                 3: self.reconstruction}
+        self.namedict = {0: "initialize", 1: "report", 2: "forward_signatures", 3: "reconstruction"}
+
+    # ------------------------------------------------------------ lifecycle
+    def kernelStarting(self, startTime):
+        for k in ("srv_report", "srv_crosscheck", "srv_reconstruction"):
+            self.kernel.custom_state[k] = pd.Timedelta(0)
+        self.setComputationDelay(0)
+        super().kernelStarting(startTime)
+
+    def kernelStopping(self):
+        for k, cat in (("srv_report", "REPORT"), ("srv_crosscheck", "CROSSCHECK"),
+                       ("srv_reconstruction", "RECONSTRUCTION")):
+            self.kernel.custom_state[k] += self.elapsed_time[cat] / self.no_of_iterations
+        super().kernelStopping()
+
+    def wakeup(self, currentTime):
+        super().wakeup(currentTime)
+        self.agent_print(f"wakeup in iteration {self.current_iteration} at function "
+                         f"{self.namedict[self.current_round]}; current time is {currentTime}")
+        self.aggProcessingMap[self.current_round](currentTime)
+
+    def receiveMessage(self, currentTime, msg):
+        super().receiveMessage(currentTime, msg)
+        body = msg.body
+        sender = body["sender"]
+        late = body.get("iteration") != self.current_iteration
+        if body["msg"] == "VECTOR":
+            if late:
+                self.logger.info(f"LATE MSG: VECTOR from iteration {body['iteration']} client {sender}")
+                return
+            self.recv_user_vectors[sender] = body["vector"]
+            self.recv_mi_cipher[sender] = json.loads(body["enc_mi_shares"])
+            for k, v in json.loads(body["enc_pairwise"]).items():
+                self.recv_pairwise_cipher[tuple(json.loads(k))] = v
+        elif body["msg"] == "SIGN":
+            if not late:
+                self.recv_committee_sigs[sender] = body["signed_labels"]
+        elif body["msg"] == "SHARED_RESULT":
+            if late:
+                self.logger.info(f"LATE MSG: SHARED_RESULT from iteration {body['iteration']} client {sender}")
+                return
+            self.recv_committee_shares_pairwise[sender] = json.loads(body["shared_result_pairwise"])
+            self.recv_committee_shares_mi[sender] = json.loads(body["shared_result_mi"])
+            self.recv_recon_index[sender] = body["committee_member_idx"]
+
+    # ---------------------------------------------------------------- round
+    def initialize(self, currentTime):
+        t0 = pd.Timestamp("now")
+        self.user_committee = param.committee(self.num_clients)
+        self.committee_threshold = int(param.fraction * len(self.user_committee))
+        # decryption-key shares for the committee (real Shamir over n; the key itself is a stand-in)
+        system_sk = int.from_bytes(hashlib.sha256(b"flm-system-sk" + param.root_seed).digest(), "big") % self.prime
+        shares = shamir_share(system_sk, max(1, self.committee_threshold), len(self.user_committee), self.prime,
+                              rng=None)
+        for cnt, cid in enumerate(sorted(self.user_committee)):
+            self.sendMessage(cid, Message({"msg": "COMMITTEE_SHARED_SK", "sender": self.id,
+                                           "committee_member_idx": cnt + 1, "sk_share": shares[cnt]}),
+                             tag="comm_dec_server")
+        self.current_round = 1
+        self.setWakeup(currentTime + (pd.Timestamp("now") - t0) + pd.Timedelta("2s"))
+
+    def report(self, currentTime):
+        t0 = pd.Timestamp("now")
+        self.report_read_from_pool()
+        self.report_process()
+        self.report_clear_pool()
+        self.report_send_message()
+        delay = pd.Timestamp("now") - t0
+        self.agent_print("run time for report step:", delay)
+        self.recordTime(t0, "REPORT")
+        self.current_round = 2
+        self.setWakeup(currentTime + delay + pd.Timedelta(P.wt_flamingo_crosscheck_ns))
+
+    def report_read_from_pool(self):
+        self.user_vectors, self.recv_user_vectors = self.recv_user_vectors, {}
+        self.mi_cipher, self.recv_mi_cipher = self.recv_mi_cipher, {}
+        self.pairwise_cipher, self.recv_pairwise_cipher = self.recv_pairwise_cipher, {}
+
+    def report_clear_pool(self):
+        self.recv_committee_shares_mi, self.recv_committee_shares_pairwise = {}, {}
+        self.recv_recon_index, self.recv_committee_sigs = {}, {}
+
+    def report_process(self):
+        self.agent_print("number of collected vectors:", len(self.user_vectors))
+        self.client_id_list = list(self.mi_cipher.keys())
+        online = set(self.user_vectors.keys())
+        offline = set(self.users) - online
+        # partial sum on the GPU (:346-350); the guard mirrors :348-349
+        for cid, v in self.user_vectors.items():
+            if len(v) != self.vector_len:
+                raise RuntimeError("Client sends vector of incorrect length.")
+        self.vec_sum_partial = param.engine().aggregate_unmask(list(self.user_vectors.values()), [], [],
+                                                              L=self.vector_len)
+        # dropout pairs (online nb, offline id) and their signs (:359-380)
+        nbrs = param.neighbors(self.current_iteration, self.num_clients, self.neighborhood_size)
+        pairs, signs = P.dropout_pairs(nbrs, online, offline)
+        self.dec_target_pairwise, self.recon_symbol = {}, {}
+        for pr, sg in zip(pairs, signs):
+            if pr not in self.pairwise_cipher:
+                raise RuntimeError("Message lost:", pr)
+            self.dec_target_pairwise[pr] = self.pairwise_cipher[pr]
+            self.recon_symbol[pr] = sg
+        labels = json.dumps(sorted(offline))
+        self.labels_and_sig = (labels, hashlib.sha256(labels.encode()).hexdigest())  # DSS stand-in
+
+    def report_send_message(self):
+        for cnt, cid in enumerate(sorted(self.user_committee)):
+            self.sendMessage(cid, Message({
+                "msg": "SIGN", "sender": self.id, "iteration": self.current_iteration,
+                "dec_target_pairwise": json.dumps({json.dumps(list(k)): v for k, v in self.dec_target_pairwise.items()}),
+                "dec_target_mi": json.dumps([self.mi_cipher[c][cnt] for c in self.client_id_list]),
+                "client_id_list": self.client_id_list, "labels": self.labels_and_sig}), tag="comm_dec_server")
+
+    def forward_signatures(self, currentTime):
+        t0 = pd.Timestamp("now")
+        self.committee_sigs = self.recv_committee_sigs
+        self.recv_committee_shares_mi = {}
+        self.recv_committee_shares_pairwise, self.recv_recon_index = {}, {}
+        for cid in sorted(self.user_committee):
+            self.sendMessage(cid, Message({"msg": "DEC", "sender": self.id, "iteration": self.current_iteration,
+                                           "labels": self.committee_sigs}), tag="comm_sign_server")
+        self.current_round = 3
+        delay = pd.Timestamp("now") - t0
+        self.agent_print("run time for crosscheck step:", delay)
+        self.setWakeup(currentTime + delay + pd.Timedelta(P.wt_flamingo_reconstruction_ns))
+        self.recordTime(t0, "CROSSCHECK")
+
+    def reconstruction(self, currentTime):
+        t0 = pd.Timestamp("now")
+        self.committee_shares_pairwise, self.recv_committee_shares_pairwise = self.recv_committee_shares_pairwise, {}
+        self.committee_shares_mi, self.recv_committee_shares_mi = self.recv_committee_shares_mi, {}
+        self.recon_index, self.recv_recon_index = self.recv_recon_index, {}
+        self.reconstruction_process()
+        self.user_vectors = {}
+        self.committee_shares_pairwise, self.committee_shares_mi, self.recon_index = {}, {}, {}
+        for uid in self.users:
+            self.sendMessage(uid, Message({"msg": "REQ", "sender": 0, "output": 1}), tag="comm_output_server")
+        delay = pd.Timestamp("now") - t0
+        self.agent_print("run time for reconstruction step:", delay)
+        self.recordTime(t0, "RECONSTRUCTION")
+        print()
+        print("######## Iteration completion ########")
+        print(f"[Server] finished iteration {self.current_iteration} at {currentTime + delay}")
+        print()
+        self.current_round = 1
+        self.current_iteration += 1
+        if self.current_iteration > self.no_of_iterations:
+            return
+        self.setWakeup(currentTime + delay + pd.Timedelta(P.wt_flamingo_report_ns))
+
+    def reconstruction_process(self):
+        self.agent_print("number of collected shares from decryptors:", len(self.committee_shares_mi))
+        if len(self.committee_shares_mi) < self.committee_threshold:
+            raise RuntimeError("No enough shares for decryption received.")
+        # m_i from the first `threshold` decryptors' shares (:506-526)
+        members = list(self.committee_shares_mi.keys())[: max(1, self.committee_threshold)]
+        xs = [self.recon_index[m] for m in members]
+        coeff = lagrange_at_zero(xs, self.prime)
+        seeds, signs = [], []
+        for pos, _cid in enumerate(self.client_id_list):
+            mi = sum(c * self.committee_shares_mi[m][pos] for c, m in zip(coeff, members)) % self.prime
+            seeds.append(mi.to_bytes(self.key_length, "big"))
+            signs.append(-1)
+        if not self.dec_target_pairwise:
+            self.agent_print("no client dropped out.")
+        else:
+            # dropout-pair seeds as returned by the decryptors, in recon_symbol order (:587-603)
+            dec = self.committee_shares_pairwise[members[0]]
+            for pr, sg in self.recon_symbol.items():
+                seeds.append(bytes.fromhex(dec[json.dumps(list(pr))]))
+                signs.append(sg)
+        # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU
+        out = self.vec_sum_partial.astype(np.uint32, copy=True)
+        self.final_sum = param.engine().mask_accumulate(seeds, signs, out)
+        self.results[self.current_iteration] = self.final_sum
+        self.agent_print("final sum:", self.final_sum)
+
+    # ----------------------------------------------------------------- util
+    def recordTime(self, startTime, categoryName):
+        self.elapsed_time[categoryName] += pd.Timestamp("now") - startTime
+
+    def agent_print(*args, **kwargs):
+        print(*args, **kwargs)

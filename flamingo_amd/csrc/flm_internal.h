@@ -72,6 +72,10 @@ enum ItemsVariant : int {
     kVarBlock = 1,      // block-layout rows, separate accumulators (any plan)
     kVarMerged = 2,     // block-layout rows added into the mask accumulator (single-tile plans)
     kVarMergedW8 = 3,   // kVarMerged at >= 8 waves/SIMD register budget
+    kVarMergedRU4 = 4,  // kVarMerged, 4 rows in flight in the rows-only loop
+    kVarMergedNT = 5,   // kVarMerged, non-temporal row loads
+    kVarMergedRU4NT = 6,
+    kVarCount = 7,
 };
 // subtiles: 1, 4 or 16 sub-tiles of 1024 slots per workgroup.
 hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_items, const uint32_t *d_rows,

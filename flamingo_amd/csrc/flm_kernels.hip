@@ -180,14 +180,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // (tail tile) come back as zero from the hardware range check, no branches.
 // BL = block layout: lane t loads its own 64 B (slots 16t..16t+15), the layout
 // the ChaCha block is generated in; otherwise coalesced layout (slot 4t + 256j).
-template <bool BL>
+// AUX = buffer cache-policy bits (0 default, 2 = nt: streamed once, MI355X_MICROARCH.md nt-weights).
+template <bool BL, int AUX = 0>
 __device__ __forceinline__ void load_row(const uint32_t *base, uint32_t bytes, int lane, u32x4 (&v)[4]) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(base), 0,
                                                                         (int)bytes, 0x00020000);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         v[j] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, BL ? 64 * lane + 16 * j : 16 * lane + 1024 * j, 0, 0));
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, BL ? 64 * lane + 16 * j : 16 * lane + 1024 * j, 0, AUX));
 }
 
 // Sum the Cw chunk partials of every sub-tile from LDS and write the tile.
@@ -233,7 +234,7 @@ __device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32
 //           rows are added straight into the mask accumulator (needs BL): one
 //           16-register accumulator instead of two, no transpose.
 //   WPE     minimum waves per SIMD requested from the register allocator.
-template <int S, bool BL, bool MERGED, int WPE>
+template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0>
 __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__restrict__ items,
                                                               const uint32_t *__restrict__ rows,
                                                               uint64_t row_pitch,
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
                                                               uint32_t *__restrict__ out) {
     static_assert(!MERGED || BL, "merged accumulation needs block-layout rows");
     constexpr int Cw = kWavesPerGroup / S;
-    constexpr int RU = MERGED ? 2 : 4;  // rows in flight per wave in the rows-only loop
+    constexpr int RU = MERGED ? RUM : 4;  // rows in flight per wave in the rows-only loop
     __shared__ u32x4 lds[kWavesPerGroup * 256];  // 64 KiB: one 4 KiB region per wave
 
     const Item it = items[blockIdx.x];
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
     const uint32_t np = nr < ns ? nr : ns;
     for (uint32_t q = 0; q < np; ++q) {
         u32x4 v[4];
-        load_row<BL>(rp, row_bytes, lane, v);
+        load_row<BL, AUX>(rp, row_bytes, lane, v);
         chacha_mask_add(rec, ctr, m);
         add_row(v);
         rp += row_pitch;
@@ -304,14 +305,14 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
     for (; rr >= RU; rr -= RU) {
         u32x4 v[RU][4];
 #pragma unroll
-        for (int u = 0; u < RU; ++u) load_row<BL>(rp + u * row_pitch, row_bytes, lane, v[u]);
+        for (int u = 0; u < RU; ++u) load_row<BL, AUX>(rp + u * row_pitch, row_bytes, lane, v[u]);
 #pragma unroll
         for (int u = 0; u < RU; ++u) add_row(v[u]);
         rp += RU * row_pitch;
     }
     for (; rr > 0; --rr) {
         u32x4 v[4];
-        load_row<BL>(rp, row_bytes, lane, v);
+        load_row<BL, AUX>(rp, row_bytes, lane, v);
         add_row(v);
         rp += row_pitch;
     }
@@ -426,10 +427,10 @@ hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, i
     return hipGetLastError();
 }
 
-template <int S, bool BL, bool MERGED, int WPE>
+template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0>
 static void launch_items_t(const Item *d_items, int n_items, const uint32_t *d_rows, uint64_t row_pitch,
                            const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out, hipStream_t stream) {
-    hipLaunchKernelGGL((items_kernel<S, BL, MERGED, WPE>), dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+    hipLaunchKernelGGL((items_kernel<S, BL, MERGED, WPE, RUM, AUX>), dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
                        row_pitch, d_recs, d_meta, d_out);
 }
 
@@ -437,13 +438,17 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
                         uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out,
                         hipStream_t stream) {
     if (n_items <= 0) return hipSuccess;
-#define FLM_L(S, BL, MG, W) launch_items_t<S, BL, MG, W>(d_items, n_items, d_rows, row_pitch, d_recs, d_meta, d_out, stream)
+#define FLM_L(S, BL, MG, W, ...) \
+    launch_items_t<S, BL, MG, W, ##__VA_ARGS__>(d_items, n_items, d_rows, row_pitch, d_recs, d_meta, d_out, stream)
 #define FLM_V(S)                                                     \
     switch (variant) {                                               \
         case kVarCoalesced: FLM_L(S, false, false, 4); break;        \
         case kVarBlock: FLM_L(S, true, false, 4); break;             \
         case kVarMerged: FLM_L(S, true, true, 4); break;             \
         case kVarMergedW8: FLM_L(S, true, true, 8); break;           \
+        case kVarMergedRU4: FLM_L(S, true, true, 4, 4, 0); break;    \
+        case kVarMergedNT: FLM_L(S, true, true, 4, 2, 2); break;     \
+        case kVarMergedRU4NT: FLM_L(S, true, true, 4, 4, 2); break;  \
         default: return hipErrorInvalidValue;                        \
     }
     switch (subtiles) {

@@ -207,7 +207,7 @@ int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     // measured (tools/ab_items.py, profiles/r01_ab_items.log): merged accumulator
     // fastest where legal, block-layout rows next
     if (v < 0) v = plan.single_tile ? flm::kVarMerged : flm::kVarBlock;
-    if (!plan.single_tile && (v == flm::kVarMerged || v == flm::kVarMergedW8)) v = flm::kVarBlock;
+    if (!plan.single_tile && v >= flm::kVarMerged) v = flm::kVarBlock;
     return v;
 }
 
@@ -650,7 +650,7 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     if (!ctx || !key) return fail(ctx, FLM_EINVAL, "NULL argument");
     const std::string k(key);
     if (k == "variant") {
-        if (value < -1 || value > flm::kVarMergedW8) return fail(ctx, FLM_EINVAL, "variant %d out of range", value);
+        if (value < -1 || value >= flm::kVarCount) return fail(ctx, FLM_EINVAL, "variant %d out of range", value);
         ctx->tune_variant = value;
     } else if (k == "subtiles") {
         if (value != 0 && value != 1 && value != 4 && value != 16)

@@ -23,10 +23,12 @@
  *     :529-536 (self masks, always subtracted), :587-603 (dropout-pair masks,
  *     sign recon_symbol), :538-540/:605 (final combine), all mod 2^32.
  *
- * Parity is pinned by the published ChaCha20 known-answer vectors (RFC 7539
- * A.1 / 2.3.2 / 2.4.2), by fixtures generated with OpenSSL's independent
- * ChaCha20 (tests/golden/make_golden.py), and by the reference's own
- * neighbour-graph probe recorded in SURVEY.md 8c.
+ * PARITY UNPINNED against the reference itself: the reference ships no
+ * tests or golden vectors, and its cipher (pycryptodomex, un-vendored) is not
+ * importable here, so no reference-produced vector exists.  Substitute pins:
+ * the published ChaCha20 vectors (RFC 7539 2.3.2 and A.1), fixtures generated
+ * with OpenSSL's independent ChaCha20 (tests/golden/make_golden.py), and the
+ * protocol invariant out == |U| (SA_ClientAgent.py:304, SA_ServiceAgent.py:605).
  */
 #include <stdint.h>
 #include <stddef.h>

@@ -20,6 +20,11 @@ Reference call sites restated (paths relative to /root/reference):
 * client masking -- agent/flamingo/SA_ClientAgent.py:304-324.
 * server aggregate + unmask -- agent/flamingo/SA_ServiceAgent.py:346-350,
   529-540, 587-605.
+
+PARITY UNPINNED against the reference itself (no reference tests/fixtures
+exist and its pycryptodomex cipher is not importable here).  Pinned instead by
+RFC 7539 vectors, OpenSSL-generated fixtures (tests/golden/) and the
+out == |U| protocol invariant; see DESIGN.md section 3.
 """
 from __future__ import annotations
 

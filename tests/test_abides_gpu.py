@@ -1,0 +1,29 @@
+"""End-to-end Flamingo simulation through the ABIDES surface with the GPU engine.
+
+The reference's only correctness oracle is the printed final sum, which equals
+|U| in every slot because client inputs are all ones (SA_ClientAgent.py:304,
+SA_ServiceAgent.py:605).  Here it is asserted, with and without dropouts."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_simulation_no_dropout():
+    from flamingo_amd.abides.config_flamingo import run
+    res = run(["-c", "flamingo", "-n", "128", "-i", "2", "-s", "7", "-k", "--root_seed_hex", "00" * 32])
+    srv = res["server"]
+    assert sorted(srv.results) == [1, 2]
+    for it, out in srv.results.items():
+        assert out.dtype == np.uint32 and out.shape == (16000,)
+        assert np.all(out == 128), it
+
+
+def test_simulation_with_dropouts():
+    from flamingo_amd.abides.config_flamingo import run
+    res = run(["-c", "flamingo", "-n", "128", "-i", "2", "-s", "11", "-k", "--offline", "3,77,100",
+               "--vector_len", "16384"])
+    srv = res["server"]
+    for it, out in srv.results.items():
+        assert np.all(out == 125), it
+    assert len(srv.recon_symbol) > 0          # dropout pairs were cancelled

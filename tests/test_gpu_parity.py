@@ -227,7 +227,7 @@ def test_full_size_invariant(eng, N, L):
     assert np.array_equal(d_rows[i, :4096].cpu().numpy().view(np.uint32), want[0])
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subtiles", [0, 1, 4, 16])
 def test_kernel_variants_bit_identical(eng, variant, subtiles):
     """Every items_kernel variant / tiling gives the oracle's bits (incl. tails, K > 256)."""

@@ -36,6 +36,46 @@ __device__ __forceinline__ void blocks(uint32_t k, uint32_t ctr, uint32_t (&acc)
         for (int i = 0; i < 16; ++i) acc[i] += x[b][i] ^ 0x64636261u;
 }
 
+// grouped schedule: the 4 independent QRs advance in lock-step, one op type per
+// group of 4, sched_barrier between groups so the compiler keeps the pattern.
+#define SB __builtin_amdgcn_sched_barrier(0);
+#define G4(OPA, OPB, OPC, OPD) OPA; OPB; OPC; OPD; SB
+#define RQ4(a0,b0,c0,d0, a1,b1,c1,d1, a2,b2,c2,d2, a3,b3,c3,d3) \
+    G4(a0 += b0, a1 += b1, a2 += b2, a3 += b3) G4(d0 ^= a0, d1 ^= a1, d2 ^= a2, d3 ^= a3) \
+    G4(d0 = ROTL(d0,16), d1 = ROTL(d1,16), d2 = ROTL(d2,16), d3 = ROTL(d3,16)) \
+    G4(c0 += d0, c1 += d1, c2 += d2, c3 += d3) G4(b0 ^= c0, b1 ^= c1, b2 ^= c2, b3 ^= c3) \
+    G4(b0 = ROTL(b0,12), b1 = ROTL(b1,12), b2 = ROTL(b2,12), b3 = ROTL(b3,12)) \
+    G4(a0 += b0, a1 += b1, a2 += b2, a3 += b3) G4(d0 ^= a0, d1 ^= a1, d2 ^= a2, d3 ^= a3) \
+    G4(d0 = ROTL(d0,8), d1 = ROTL(d1,8), d2 = ROTL(d2,8), d3 = ROTL(d3,8)) \
+    G4(c0 += d0, c1 += d1, c2 += d2, c3 += d3) G4(b0 ^= c0, b1 ^= c1, b2 ^= c2, b3 ^= c3) \
+    G4(b0 = ROTL(b0,7), b1 = ROTL(b1,7), b2 = ROTL(b2,7), b3 = ROTL(b3,7))
+
+__device__ __forceinline__ void block_grouped(uint32_t k, uint32_t ctr, uint32_t (&acc)[16]) {
+    uint32_t x0,x1,x2,x3,x4,x5,x6,x7,x8,x9,x10,x11,x12,x13,x14,x15;
+    x0=k;x1=k*2;x2=k*3;x3=k*4;x4=k*5;x5=k*6;x6=k*7;x7=k*8;x8=k*9;x9=k*10;x10=k*11;x11=k*12;x12=ctr;x13=k*14;x14=k*15;x15=k*16;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        RQ4(x0,x4,x8,x12, x1,x5,x9,x13, x2,x6,x10,x14, x3,x7,x11,x15)
+        RQ4(x0,x5,x10,x15, x1,x6,x11,x12, x2,x7,x8,x13, x3,x4,x9,x14)
+    }
+    acc[0]+=x0^0x64636261u; acc[1]+=x1^0x64636261u; acc[2]+=x2^0x64636261u; acc[3]+=x3^0x64636261u;
+    acc[4]+=x4^0x64636261u; acc[5]+=x5^0x64636261u; acc[6]+=x6^0x64636261u; acc[7]+=x7^0x64636261u;
+    acc[8]+=x8^0x64636261u; acc[9]+=x9^0x64636261u; acc[10]+=x10^0x64636261u; acc[11]+=x11^0x64636261u;
+    acc[12]+=x12^0x64636261u; acc[13]+=x13^0x64636261u; acc[14]+=x14^0x64636261u; acc[15]+=x15^0x64636261u;
+}
+
+__global__ __launch_bounds__(256) void probe_grouped(int iters, uint32_t *out) {
+    uint32_t acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0;
+    const uint32_t ctr = blockIdx.x * 256 + threadIdx.x;
+    for (int it = 0; it < iters; ++it) block_grouped(0x9e3779b9u * (it + 1), ctr, acc);
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s ^= acc[i];
+    out[ctr] = s;
+}
+
 template <int NB, int WPS>
 __global__ __launch_bounds__(256, WPS) void probe(int iters, uint32_t *out) {
     uint32_t acc[16];
@@ -89,6 +129,8 @@ int main() {
         float t2 = timeit([&] { hipLaunchKernelGGL((probe<2, 1>), dim3(grid), dim3(256), 0, 0, iters, out); });
         float t1o = timeit([&] { hipLaunchKernelGGL((probe<1, 2>), dim3(grid), dim3(256), 0, 0, iters, out); });
         float t2o = timeit([&] { hipLaunchKernelGGL((probe<2, 2>), dim3(grid), dim3(256), 0, 0, iters, out); });
+        float tg = timeit([&] { hipLaunchKernelGGL(probe_grouped, dim3(grid), dim3(256), 0, 0, iters, out); });
+        printf("grid %5d  grouped %.3f ms %.1f Gw/s\n", grid, tg, words / tg / 1e6);
         printf("grid %5d  NB1 %.3f ms %.1f Gw/s | NB2 %.3f ms %.1f Gw/s | NB1,w2 %.3f ms %.1f | NB2,w2 %.3f ms %.1f\n", grid,
                t1, words / t1 / 1e6, t2, words / t2 / 1e6, t1o, words / t1o / 1e6, t2o, words / t2o / 1e6);
     }
