@@ -184,6 +184,10 @@ def main():
                           "frac": round(valu_tops / VALU_PEAK_TOPS, 4)},
     }
 
+    tr = committed_traffic(rows_rank, L, int(K))
+    if tr is not None:
+        res["roofline"]["traffic"] = tr["bytes"]
+        res["roofline"]["traffic_source"] = tr["source"]
     if rank == 0 and G == 1 and not args.profile:
         if not args.no_variants:
             res["variants"] = variant_pairs_only(eng, torch, rows_on, m, nbrs, online, L, stream, P)
@@ -197,6 +201,26 @@ def main():
         dist.destroy_process_group()
     eng.close()
     return 0 if ok else 1
+
+
+def committed_traffic(rows, L, K):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/*_profile_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when the
+    profiled command was this same workload; None otherwise."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_profile_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        wl = d.get("workload", {"rows": 1024, "L": 1 << 20, "K": 1024})
+        if (wl.get("rows"), wl.get("L"), wl.get("K")) != (rows, L, K):
+            continue
+        for k, v in d.get("counters", {}).items():
+            if k.startswith("flm::items_kernel<1") and "hbm_traffic_bytes" in v:
+                best = {"bytes": int(v["hbm_traffic_bytes"]), "source": os.path.relpath(f, ROOT)}
+    return best
 
 
 def variant_pairs_only(eng, torch, rows, m, nbrs, online, L, stream, P):

@@ -66,6 +66,7 @@ class SA_ServiceAgent(Agent):
         self.current_iteration = 1
         self.current_round = 0
         self.results = {}            # iteration -> final_sum (kept for inspection / tests)
+        self.online_counts = {}      # iteration -> |U|
         self.aggProcessingMap = {0: self.initialize, 1: self.report, 2: self.forward_signatures,
                                  3: self.reconstruction}
         self.namedict = {0: "initialize", 1: "report", 2: "forward_signatures", 3: "reconstruction"}
@@ -201,8 +202,7 @@ class SA_ServiceAgent(Agent):
         self.committee_shares_mi, self.recv_committee_shares_mi = self.recv_committee_shares_mi, {}
         self.recon_index, self.recv_recon_index = self.recv_recon_index, {}
         self.reconstruction_process()
-        self.user_vectors = {}
-        self.committee_shares_pairwise, self.committee_shares_mi, self.recon_index = {}, {}, {}
+        self.reconstruction_clear_pool()
         for uid in self.users:
             self.sendMessage(uid, Message({"msg": "REQ", "sender": 0, "output": 1}), tag="comm_output_server")
         delay = pd.Timestamp("now") - t0
@@ -217,6 +217,12 @@ class SA_ServiceAgent(Agent):
         if self.current_iteration > self.no_of_iterations:
             return
         self.setWakeup(currentTime + delay + pd.Timedelta(P.wt_flamingo_report_ns))
+
+    def reconstruction_clear_pool(self):
+        # (:488-497) late messages of this iteration must not leak into the next one
+        self.user_vectors = {}
+        self.committee_shares_pairwise, self.committee_shares_mi, self.recon_index = {}, {}, {}
+        self.recv_pairwise_cipher, self.recv_mi_cipher, self.recv_user_vectors = {}, {}, {}
 
     def reconstruction_process(self):
         self.agent_print("number of collected shares from decryptors:", len(self.committee_shares_mi))
@@ -243,6 +249,7 @@ class SA_ServiceAgent(Agent):
         out = self.vec_sum_partial.astype(np.uint32, copy=True)
         self.final_sum = param.engine().mask_accumulate(seeds, signs, out)
         self.results[self.current_iteration] = self.final_sum
+        self.online_counts[self.current_iteration] = len(self.user_vectors)
         self.agent_print("final sum:", self.final_sum)
 
     # ----------------------------------------------------------------- util

@@ -143,7 +143,9 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              2 merged accumulator | 3 merged, 8 waves/SIMD budget
  *              (2/3 apply only to plans whose items each write one tile)
  *   "subtiles" 0 auto | 1 | 4 | 16 sub-tiles of 1024 slots per workgroup
- *              for aggregate plans. */
+ *              for aggregate plans.
+ *   "pairing"  0 interleaved single-kind items | 1 dual-tile items (default), for
+ *              windows where rows and masks cover different tiles. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Allocate / free page-locked host memory through HIP (for a pinned arena

@@ -254,13 +254,16 @@ def test_sharded_windows_variants(eng):
     lo, hi = 2048, 6144
     want = want_rows.copy()
     want[lo:hi] += O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds, signs, L=hi - lo, slot0=lo)
-    for v in (-1, 0, 1, 2):
-        eng.set_tuning("variant", v)
-        out = torch.empty(L, dtype=torch.int32, device="cuda")
-        eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi)
-        torch.cuda.synchronize()
-        assert np.array_equal(out.cpu().numpy().view(np.uint32), want), v
+    for pairing in (0, 1):
+        eng.set_tuning("pairing", pairing)
+        for v in (-1, 0, 1, 2, 5):
+            eng.set_tuning("variant", v)
+            out = torch.empty(L, dtype=torch.int32, device="cuda")
+            eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want), (pairing, v)
     eng.set_tuning("variant", -1)
+    eng.set_tuning("pairing", 1)
     # empty shard (rank owning no slots) with an unaligned clipped bound
     out = torch.empty(L, dtype=torch.int32, device="cuda")
     eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=L, mask_hi=L)

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--workloads", default="full,pairs,shard8")
     ap.add_argument("--variants", default="coalesced,block,merged,merged_w8")
     ap.add_argument("--subtiles", default="1,4")
+    ap.add_argument("--pairing", default="0")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     eng = MaskEngine(0)
@@ -49,11 +50,13 @@ def main():
         eng.seed_table_dev(seeds, signs, stream=s)
         times = {}
         ref = None
-        combos = [(v, st) for v in args.variants.split(",") for st in map(int, args.subtiles.split(","))]
+        combos = [(v, st, pa) for v in args.variants.split(",") for st in map(int, args.subtiles.split(","))
+                  for pa in map(int, args.pairing.split(","))]
         for rnd in range(args.rounds):
-            for v, st in combos:
+            for v, st, pa in combos:
                 eng.set_tuning("variant", VARIANTS[v])
                 eng.set_tuning("subtiles", st)
+                eng.set_tuning("pairing", pa)
                 eng.aggregate_dev(rows, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=s)  # warm / plan
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
                 e[0].record(s)
@@ -62,17 +65,17 @@ def main():
                     e[r + 1].record(s)
                 torch.cuda.synchronize()
                 ms = [e[i].elapsed_time(e[i + 1]) for i in range(args.reps)]
-                times.setdefault((v, st), []).extend(ms)
+                times.setdefault((v, st, pa), []).extend(ms)
                 o = out.cpu().numpy()
                 if ref is None:
                     ref = o.copy()
                 elif not np.array_equal(ref, o):
-                    print(f"MISMATCH {wl} {v} st={st}", flush=True)
+                    print(f"MISMATCH {wl} {v} st={st} pairing={pa}", flush=True)
                 plan = eng.last_plan()
-        for (v, st), ms in times.items():
+        for (v, st, pa), ms in times.items():
             med, mn = float(np.median(ms)), float(np.min(ms))
             gbs = (4.0 * N * L + 4.0 * L) / (med * 1e-3) / 1e9
-            r = {"workload": wl, "variant": v, "subtiles": st, "median_ms": round(med, 4), "min_ms": round(mn, 4),
+            r = {"workload": wl, "variant": v, "subtiles": st, "pairing": pa, "median_ms": round(med, 4), "min_ms": round(mn, 4),
                  "GB/s": round(gbs, 1)}
             res.append(r)
             print(json.dumps(r), flush=True)

@@ -68,6 +68,8 @@ def main():
             cs["hbm_traffic_bytes"] = cs["hbm_read_bytes_corrected"] + cs["hbm_write_bytes"]
     for k, v in durations.items():
         res["kernels"].setdefault(k, {})["trace_avg_ns"] = sum(v) / len(v)
+    res["workload"] = {"rows": 1024, "L": 1 << 20, "K": 1024,
+                       "command": "python3 bench.py --profile --steps 20 --warmup 3"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1)[:4000])
 
