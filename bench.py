@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-copy", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")
     ap.add_argument("--profile", action="store_true", help="minimal run for rocprofv3 (no CPU/copy legs)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (c2, c3, c5)")
     return ap.parse_args()
 
 
@@ -191,6 +192,12 @@ def main():
     if rank == 0 and G == 1 and not args.profile:
         if not args.no_variants:
             res["variants"] = variant_pairs_only(eng, torch, rows_on, m, nbrs, online, L, stream, P)
+        if not args.no_configs:
+            res["other_configs"] = {
+                "c2": measure_config(eng, torch, P, "c2", N=128, L=16384, o=1, dropout=0.0, check_oracle=True),
+                "c3": measure_config(eng, torch, P, "c3", N=1024, L=1 << 18, o=2, dropout=0.0),
+                "c5": measure_config(eng, torch, P, "c5", N=4096, L=1 << 20, o=1, dropout=0.01, rounds=10),
+            }
         if not args.no_copy:
             res["with_copy"] = with_copy(eng, torch, rows_on, sseeds, ssigns, L, len(online))
         if not args.no_cpu:
@@ -201,6 +208,55 @@ def main():
         dist.destroy_process_group()
     eng.close()
     return 0 if ok else 1
+
+
+def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False):
+    """One BASELINE config on this GPU: valid masked rows built on the GPU, `rounds` iterations
+    (each its own neighbour graph and, with dropouts, its own offline set: PCG64(seed=iteration)),
+    `steps` timed device-resident rounds per iteration; out == |U| checked every iteration."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    m = np.frombuffer(b"".join(P.bench_seed(name, i) for i in range(N)), np.uint8).reshape(N, 32)
+    stream = torch.cuda.current_stream()
+    rows = torch.empty((N, L), dtype=torch.int32, device=dev)
+    out = torch.empty(L, dtype=torch.int32, device=dev)
+    per_round, ok_all, Ks, Ds, oks = [], True, [], [], []
+    for it in range(1, rounds + 1):
+        nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
+        seg, cs, csg = P.client_seed_table(m, nbrs, P.synthetic_pair_seed)
+        eng.client_mask_dev(seg, torch.from_numpy(cs).to(dev), csg, rows, L, stream=stream)
+        n_off = int(round(dropout * N))
+        off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, n_off, replace=False)) if n_off else \
+            np.zeros(0, np.int64)
+        on = np.setdiff1d(np.arange(N), off)
+        ss, sg = P.server_seed_table(m, nbrs, on, off, P.synthetic_pair_seed)
+        r_on = rows if len(on) == N else rows[torch.from_numpy(on).to(dev)].contiguous()
+        d_s, d_g = torch.from_numpy(ss).to(dev), torch.from_numpy(sg).to(dev)
+        for _ in range(2):
+            eng.aggregate_unmask_dev(r_on, d_s, d_g, out, L=L, stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            eng.aggregate_unmask_dev(r_on, d_s, d_g, out, L=L, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        per_round.append(e0.elapsed_time(e1) / steps)
+        ok = bool(torch.all(out == len(on)).item())
+        if check_oracle:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O  # checker only
+            want = O.aggregate_unmask(r_on.cpu().numpy().view(np.uint32), ss, sg, threads=8)
+            ok = ok and bool(np.array_equal(want, out.cpu().numpy().view(np.uint32)))
+        ok_all &= ok
+        Ks.append(int(ss.shape[0]))
+        Ds.append(int(ss.shape[0] - len(on)))
+        oks.append(int(len(on)))
+        del r_on
+    ms = float(np.mean(per_round))
+    nu = float(np.mean(oks))
+    return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
+            "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
+            "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
+            "correct": ok_all, "checked_against_oracle": bool(check_oracle)}
 
 
 def committed_traffic(rows, L, K):
