@@ -41,6 +41,8 @@ SIGNATURES = {
     "flm_last_plan": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
     "flm_set_tuning": (_int, [_vp, ctypes.c_char_p, _int]),
+    "flm_plan_aggregate": (_int, [_int, _int, _sz, _int, _int, _sz, _sz, _sz, _u64, _vp, _int,
+                                  ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }

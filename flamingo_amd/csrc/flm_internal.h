@@ -75,7 +75,9 @@ enum ItemsVariant : int {
     kVarMergedRU4 = 4,  // kVarMerged, 4 rows in flight in the rows-only loop
     kVarMergedNT = 5,   // kVarMerged, non-temporal row loads
     kVarMergedRU4NT = 6,
-    kVarCount = 7,
+    kVarMergedSpread = 7,  // kVarMerged, seeds spread evenly over the row stream
+    kVarBlockSpread = 8,   // kVarBlock (dual-tile plans), seeds spread over the row stream
+    kVarCount = 9,
 };
 // subtiles: 1, 4 or 16 sub-tiles of 1024 slots per workgroup.
 hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_items, const uint32_t *d_rows,

@@ -234,7 +234,7 @@ __device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32
 //           rows are added straight into the mask accumulator (needs BL): one
 //           16-register accumulator instead of two, no transpose.
 //   WPE     minimum waves per SIMD requested from the register allocator.
-template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0>
+template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0, bool SPREAD = false>
 __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__restrict__ items,
                                                               const uint32_t *__restrict__ rows,
                                                               uint64_t row_pitch,
@@ -290,36 +290,58 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         }
     };
 
-    // paired phase: one row load in flight under one ChaCha block per step
-    const uint32_t np = nr < ns ? nr : ns;
-    for (uint32_t q = 0; q < np; ++q) {
-        u32x4 v[4];
-        load_row<BL, AUX>(rp, row_bytes, lane, v);
-        chacha_mask_add(rec, ctr, m);
-        add_row(v);
-        rp += row_pitch;
-        ++rec;
-    }
-    // remaining rows: RU rows (RU x 4 KiB per wave) in flight
-    uint32_t rr = nr - np;
-    for (; rr >= RU; rr -= RU) {
-        u32x4 v[RU][4];
+    if constexpr (SPREAD) {
+        // seeds spread evenly over the row stream (Bresenham): every row load is
+        // issued before the ChaCha block that hides it, and seed-light items keep
+        // HBM busy from the first row instead of front-loading the VALU work
+        uint32_t q = 0;
+        for (uint32_t r = 0; r < nr; ++r) {
+            u32x4 v[4];
+            load_row<BL, AUX>(rp, row_bytes, lane, v);
+            if (q < ns && (uint64_t)q * nr <= (uint64_t)r * ns) {
+                chacha_mask_add(rec, ctr, m);
+                ++rec;
+                ++q;
+            }
+            add_row(v);
+            rp += row_pitch;
+        }
+        for (; q < ns; ++q) {
+            chacha_mask_add(rec, ctr, m);
+            ++rec;
+        }
+    } else {
+        // paired phase: one row load in flight under one ChaCha block per step
+        const uint32_t np = nr < ns ? nr : ns;
+        for (uint32_t q = 0; q < np; ++q) {
+            u32x4 v[4];
+            load_row<BL, AUX>(rp, row_bytes, lane, v);
+            chacha_mask_add(rec, ctr, m);
+            add_row(v);
+            rp += row_pitch;
+            ++rec;
+        }
+        // remaining rows: RU rows (RU x 4 KiB per wave) in flight
+        uint32_t rr = nr - np;
+        for (; rr >= RU; rr -= RU) {
+            u32x4 v[RU][4];
 #pragma unroll
-        for (int u = 0; u < RU; ++u) load_row<BL, AUX>(rp + u * row_pitch, row_bytes, lane, v[u]);
+            for (int u = 0; u < RU; ++u) load_row<BL, AUX>(rp + u * row_pitch, row_bytes, lane, v[u]);
 #pragma unroll
-        for (int u = 0; u < RU; ++u) add_row(v[u]);
-        rp += RU * row_pitch;
-    }
-    for (; rr > 0; --rr) {
-        u32x4 v[4];
-        load_row<BL, AUX>(rp, row_bytes, lane, v);
-        add_row(v);
-        rp += row_pitch;
-    }
-    // remaining seeds
-    for (uint32_t q = np; q < ns; ++q) {
-        chacha_mask_add(rec, ctr, m);
-        ++rec;
+            for (int u = 0; u < RU; ++u) add_row(v[u]);
+            rp += RU * row_pitch;
+        }
+        for (; rr > 0; --rr) {
+            u32x4 v[4];
+            load_row<BL, AUX>(rp, row_bytes, lane, v);
+            add_row(v);
+            rp += row_pitch;
+        }
+        // remaining seeds
+        for (uint32_t q = np; q < ns; ++q) {
+            chacha_mask_add(rec, ctr, m);
+            ++rec;
+        }
     }
 
     // ---- combine through this wave's LDS region (natural slot order), then
@@ -427,10 +449,10 @@ hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, i
     return hipGetLastError();
 }
 
-template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0>
+template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0, bool SPREAD = false>
 static void launch_items_t(const Item *d_items, int n_items, const uint32_t *d_rows, uint64_t row_pitch,
                            const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out, hipStream_t stream) {
-    hipLaunchKernelGGL((items_kernel<S, BL, MERGED, WPE, RUM, AUX>), dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
+    hipLaunchKernelGGL((items_kernel<S, BL, MERGED, WPE, RUM, AUX, SPREAD>), dim3(n_items), dim3(kThreads), 0, stream, d_items, d_rows,
                        row_pitch, d_recs, d_meta, d_out);
 }
 
@@ -449,6 +471,8 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
         case kVarMergedRU4: FLM_L(S, true, true, 4, 4, 0); break;    \
         case kVarMergedNT: FLM_L(S, true, true, 4, 2, 2); break;     \
         case kVarMergedRU4NT: FLM_L(S, true, true, 4, 4, 2); break;  \
+        case kVarMergedSpread: FLM_L(S, true, true, 4, 2, 0, true); break; \
+        case kVarBlockSpread: FLM_L(S, true, false, 4, 2, 0, true); break; \
         default: return hipErrorInvalidValue;                        \
     }
     switch (subtiles) {

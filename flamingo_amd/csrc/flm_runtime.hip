@@ -68,6 +68,7 @@ struct Plan {
     bool needs_zero = false;
     int atomics = 0;
     bool single_tile = true;  // every item writes one tile (merged accumulator legal)
+    bool seed_light = false;  // mask work small next to row streaming
 };
 
 using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>;
@@ -243,10 +244,11 @@ int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t ns
 
 int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     int v = ctx->tune_variant;
-    // measured (tools/ab_items.py, profiles/r01_ab_items.log): merged accumulator
-    // fastest where legal, block-layout rows next
-    if (v < 0) v = plan.single_tile ? flm::kVarMerged : flm::kVarBlock;
-    if (!plan.single_tile && v >= flm::kVarMerged) v = flm::kVarBlock;
+    // measured (tools/ab_items.py, profiles/r01_ab_items*.log): merged accumulator
+    // fastest where legal (seeds spread over the rows when seed-light), block next
+    if (v < 0) v = plan.single_tile ? (plan.seed_light ? flm::kVarMergedSpread : flm::kVarMerged) : flm::kVarBlock;
+    if (!plan.single_tile && v >= flm::kVarMerged) v = (v == flm::kVarMergedSpread || v == flm::kVarBlockSpread)
+                                                          ? flm::kVarBlockSpread : flm::kVarBlock;
     return v;
 }
 
@@ -258,16 +260,16 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
     return 0;
 }
 
-Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
-                     uint64_t prg_slot0, int *rc) {
+// Host-only planning of one aggregate round (no device state): fills `items`
+// and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
+// diagnostic entry point.
+void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo,
+                           uint64_t mask_hi, uint64_t prg_slot0, std::vector<Item> &items, Plan &plan) {
     // ChaCha-heavy rounds keep 1024-slot tiles (16 waves split one tile's seeds);
     // row-streaming-heavy rounds (few seeds per slot) prefer 4 sub-tiles per
     // workgroup: 4096-slot tiles, fewer LDS combines (measured 5.77 vs 5.26 TB/s).
     const bool seed_light = (uint64_t)K * (mask_hi - mask_lo) * 2 < (uint64_t)N * L;
-    const int subtiles = ctx->tune_subtiles > 0 ? ctx->tune_subtiles : (seed_light ? 4 : 1);
-    PlanKey key{subtiles + 100 * ctx->tune_pairing, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
-    auto f = ctx->plans.find(key);
-    if (f != ctx->plans.end()) { *rc = 0; return f->second; }
+    const int subtiles = tune_subtiles > 0 ? tune_subtiles : (seed_light ? 4 : 1);
     const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
     Job j;
     j.nrows = (uint32_t)N;
@@ -281,11 +283,21 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
     const uint64_t tm = (K > 0 && mask_hi > mask_lo) ? (mask_hi - mask_lo + W - 1) / W : 0;
     int pr, pm;
     choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm);
+    plan.subtiles = subtiles;
+    plan.seed_light = seed_light;
+    plan_job(j, pitch, subtiles, pr, pm, pairing == 1, items, plan.needs_zero, plan.atomics, plan.single_tile);
+}
+
+Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
+                     uint64_t prg_slot0, int *rc) {
+    PlanKey key{ctx->tune_subtiles + 100 * ctx->tune_pairing, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi,
+                prg_slot0};
+    auto f = ctx->plans.find(key);
+    if (f != ctx->plans.end()) { *rc = 0; return f->second; }
     std::vector<Item> items;
     Plan *plan = new Plan();
-    plan->subtiles = subtiles;
-    plan_job(j, pitch, subtiles, pr, pm, ctx->tune_pairing == 1, items, plan->needs_zero, plan->atomics,
-             plan->single_tile);
+    build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items,
+                          *plan);
     *rc = upload_plan(ctx, *plan, items);
     if (*rc) { plan->items.release(); delete plan; return nullptr; }
     if (ctx->plans.size() > 64) {  // bound the cache
@@ -683,6 +695,23 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
                                           ctx->stream));
     FLM_HIP(ctx, hipMemcpyAsync(out, ctx->bytes_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
     FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flm_plan_aggregate(int subtiles, int pairing, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,
+                       size_t mask_hi, uint64_t prg_slot0, void *items_out, int max_items, int *n_items,
+                       int *plan_flags) {
+    if (N < 0 || K < 0 || mask_hi > L || mask_lo > mask_hi || !n_items)
+        return fail(nullptr, FLM_EINVAL, "flm_plan_aggregate: bad arguments");
+    std::vector<Item> items;
+    Plan plan;
+    build_aggregate_items(subtiles, pairing, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items, plan);
+    *n_items = (int)items.size();
+    if (plan_flags)
+        *plan_flags = (plan.needs_zero ? 1 : 0) | (plan.atomics ? 2 : 0) | (plan.single_tile ? 4 : 0) |
+                      (plan.seed_light ? 8 : 0) | (plan.subtiles << 8);
+    if (items_out && max_items > 0)
+        std::memcpy(items_out, items.data(), sizeof(Item) * (size_t)std::min<int>(max_items, (int)items.size()));
     return 0;
 }
 

@@ -148,6 +148,15 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              windows where rows and masks cover different tiles. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
+/* Host-only view of the launch planner (no GPU needed): the work items the
+ * aggregate kernel would run for this round shape.  items_out receives up to
+ * max_items 64-byte items (layout: flm_internal.h Item); *n_items the total;
+ * *plan_flags bit0 zero-fill, bit1 atomics, bit2 single-tile, bit3 seed-light,
+ * bits 8.. sub-tiles per workgroup.  subtiles/pairing as flm_set_tuning. */
+int flm_plan_aggregate(int subtiles, int pairing, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,
+                       size_t mask_hi, uint64_t prg_slot0, void *items_out, int max_items, int *n_items,
+                       int *plan_flags);
+
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */
 void *flm_host_alloc(size_t bytes);

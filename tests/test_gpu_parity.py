@@ -227,7 +227,7 @@ def test_full_size_invariant(eng, N, L):
     assert np.array_equal(d_rows[i, :4096].cpu().numpy().view(np.uint32), want[0])
 
 
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("subtiles", [0, 1, 4, 16])
 def test_kernel_variants_bit_identical(eng, variant, subtiles):
     """Every items_kernel variant / tiling gives the oracle's bits (incl. tails, K > 256)."""
@@ -256,7 +256,7 @@ def test_sharded_windows_variants(eng):
     want[lo:hi] += O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds, signs, L=hi - lo, slot0=lo)
     for pairing in (0, 1):
         eng.set_tuning("pairing", pairing)
-        for v in (-1, 0, 1, 2, 5):
+        for v in (-1, 0, 1, 2, 5, 7, 8):
             eng.set_tuning("variant", v)
             out = torch.empty(L, dtype=torch.int32, device="cuda")
             eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi)
