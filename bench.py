@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")
     ap.add_argument("--profile", action="store_true", help="minimal run for rocprofv3 (no CPU/copy legs)")
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (c2, c3, c5)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL; the real multi-GPU path) or gloo (test only: ranks sharing one GPU)")
     return ap.parse_args()
 
 
@@ -61,8 +63,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev_id = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_id)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_id))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     if args.gpus != world and not (world == 1 and args.gpus == 1):
@@ -142,8 +148,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if G > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kms = float(np.mean([a.elapsed_time(b) for a, b in kern_ms]))
@@ -152,7 +159,7 @@ def main():
     out = rnd.exchange() if G > 1 else rnd.partial[:L]
     torch.cuda.synchronize()
     ok = bool(torch.all(out == len(online)).item())
-    okt = torch.tensor([1 if ok else 0], device=dev)
+    okt = torch.tensor([1 if ok else 0], device=coll_dev)
     if G > 1:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     ok = bool(okt.item())

@@ -69,7 +69,14 @@ class ShardedRound:
     def exchange(self):
         if self.world == 1:
             return self.partial[: self.L]
-        dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM, group=self.group)
+        if self.partial.is_cuda and dist.get_backend(self.group) == "gloo":
+            # test path only (several ranks sharing one GPU, where RCCL refuses duplicate
+            # devices): the same reduce-scatter on host copies
+            cpu_out = torch.empty(self.out.shape, dtype=self.out.dtype)
+            dist.reduce_scatter_tensor(cpu_out, self.partial.cpu(), op=dist.ReduceOp.SUM, group=self.group)
+            self.out.copy_(cpu_out)
+        else:
+            dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM, group=self.group)
         return self.out[: self.hi - self.lo]
 
     def step(self, d_rows, d_seeds, d_signs, stream=None):
