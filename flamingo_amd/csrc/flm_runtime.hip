@@ -79,7 +79,12 @@ struct flm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out, items_tmp;
+    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out;
+    // pinned staging ring for pageable host rows: two buffers, each reused once
+    // the DMA that read it has completed (event per buffer)
+    void *stage[2] = {nullptr, nullptr};
+    size_t stage_cap = 0;
+    hipEvent_t stage_done[2] = {nullptr, nullptr};
     std::map<PlanKey, Plan *> plans;
     Plan scratch_plan;  // uncached plans (client masking, expansion)
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
@@ -347,12 +352,72 @@ int run_plan(flm_ctx *ctx, const Plan &plan, const uint32_t *d_rows, uint64_t pi
 }
 
 // Upload N host rows (pageable or pinned) into the context's row buffer at `pitch`.
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory is not an error here
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Upload N host rows into the context's row buffer at `pitch`.  Page-locked
+// rows (e.g. from flm_host_alloc / PinnedArena) are DMA'd directly; pageable
+// rows are packed into a pinned staging ring (kStageBytes per buffer, two
+// buffers) so the copy engine sees few large transfers while the CPU fills
+// the other buffer.  The VECTOR bodies of the reference are pageable numpy
+// arrays (SA_ServiceAgent.py:210).
+constexpr size_t kStageBytes = 32u << 20;
+
 int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint64_t pitch) {
     FLM_HIP(ctx, ctx->rows.reserve(std::max<size_t>(1, (size_t)N) * pitch * sizeof(uint32_t)));
+    uint32_t *dst = ctx->rows.as<uint32_t>();
+    const size_t row_bytes = L * sizeof(uint32_t);
+    const size_t slot_bytes = pitch * sizeof(uint32_t);
+    std::vector<int> pageable;
     for (int i = 0; i < N; ++i) {
         if (!rows[i]) return fail(ctx, FLM_EINVAL, "row %d is NULL", i);
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->rows.as<uint32_t>() + (size_t)i * pitch, rows[i], L * sizeof(uint32_t),
+        if (host_pinned(rows[i]))
+            FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)i * pitch, rows[i], row_bytes, hipMemcpyHostToDevice, ctx->stream));
+        else
+            pageable.push_back(i);
+    }
+    if (pageable.empty()) return 0;
+    if (slot_bytes > kStageBytes) {  // very long rows: one DMA per row through HIP's own staging
+        for (int i : pageable)
+            FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)i * pitch, rows[i], row_bytes, hipMemcpyHostToDevice, ctx->stream));
+        return 0;
+    }
+    if (ctx->stage_cap < kStageBytes) {
+        for (int b = 0; b < 2; ++b) {
+            if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
+            ctx->stage[b] = nullptr;
+            FLM_HIP(ctx, hipHostMalloc(&ctx->stage[b], kStageBytes, hipHostMallocDefault));
+            if (!ctx->stage_done[b]) FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->stage_done[b], hipEventDisableTiming));
+        }
+        ctx->stage_cap = kStageBytes;
+    }
+    const size_t per_buf = kStageBytes / slot_bytes;  // rows per staging buffer
+    size_t k = 0;
+    int b = 0;
+    bool used[2] = {false, false};
+    while (k < pageable.size()) {
+        if (used[b]) FLM_HIP(ctx, hipEventSynchronize(ctx->stage_done[b]));  // DMA out of this buffer done
+        uint8_t *st = static_cast<uint8_t *>(ctx->stage[b]);
+        // a run of consecutive row indices packs into one contiguous device range
+        const int first = pageable[k];
+        size_t n = 0;
+        while (k + n < pageable.size() && n < per_buf && pageable[k + n] == first + (int)n) {
+            std::memcpy(st + n * slot_bytes, rows[pageable[k + n]], row_bytes);
+            ++n;
+        }
+        FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)first * pitch, st, n * slot_bytes - (slot_bytes - row_bytes),
                                     hipMemcpyHostToDevice, ctx->stream));
+        FLM_HIP(ctx, hipEventRecord(ctx->stage_done[b], ctx->stream));
+        used[b] = true;
+        k += n;
+        b ^= 1;
     }
     return 0;
 }
@@ -475,8 +540,12 @@ void flm_free(flm_ctx *ctx) {
     }
     ctx->scratch_plan.items.release();
     for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
-                      &ctx->bytes_out, &ctx->items_tmp})
+                      &ctx->bytes_out})
         b->release();
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
+        if (ctx->stage_done[i]) (void)hipEventDestroy(ctx->stage_done[i]);
+    }
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -269,3 +269,23 @@ def test_sharded_windows_variants(eng):
     eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=L, mask_hi=L)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want_rows)
+
+
+def test_host_rows_pinned_and_pageable_mix(eng):
+    """VECTOR bodies may be pageable numpy arrays or live in the pinned arena; both upload paths
+    (staging ring, direct DMA) and their interleaving give the oracle's bits."""
+    from flamingo_amd import PinnedArena
+    for N, L in ((300, 16000), (9, 3 * 2**20 + 5), (40, 17)):
+        rows, seeds, signs = rand_case(N + L, N, 5, L)
+        arena = PinnedArena(N * L * 4 + 4096 * N)
+        vecs = []
+        for i in range(N):
+            if i % 3 == 1:
+                a = arena.array((L,), np.uint32)
+                a[:] = rows[i]
+                vecs.append(a)
+            else:
+                vecs.append(rows[i].copy())
+        want = O.aggregate_unmask(rows, seeds, signs, threads=8)
+        assert np.array_equal(eng.aggregate_unmask(vecs, seeds, signs, L=L), want), (N, L)
+        arena.free()
