@@ -43,6 +43,9 @@ SIGNATURES = {
     "flm_set_tuning": (_int, [_vp, ctypes.c_char_p, _int]),
     "flm_plan_aggregate": (_int, [_int, _int, _sz, _int, _int, _sz, _sz, _sz, _u64, _vp, _int,
                                   ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "flm_ec_combine": (_int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, _u32p]),
+    "flm_ec_combine_dev": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _vp, _vp, _vp, _vp]),
+    "flm_ec_mul": (_int, [_vp, _u8p, _u8p, _int, _u8p, _u32p]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }

@@ -86,4 +86,10 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
                                const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
 
+// P-256 (flm_p256.hip). d_jac holds T*D Jacobian results as SoA planes [T][24][D].
+hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream);
+hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T, int D, int negate,
+                            uint8_t *d_points_out, uint8_t *d_digests_out, uint32_t *d_flags, hipStream_t stream);
+
 }  // namespace flm

@@ -1,0 +1,505 @@
+// flm_p256.hip -- P-256 batch kernels for Flamingo's seed recovery (gfx950).
+//
+// The server recovers every dropped pair's seed from the committee's threshold
+// ElGamal decryption shares (SA_ServiceAgent.py:542-585):
+//     point_i = c1_i - sum_j lambda_j * share_{j,i}          (share = sk_j * c0_i)
+//     seed_i  = SHA-256(x(point_i) || y(point_i))            (32-byte big endian)
+// and the clients/committee do single scalar multiplications (ECDH :256-263,
+// ElGamal :434-447, decryption shares :397-400).  All of it is 256-bit modular
+// arithmetic on independent points -- one lane per (term, pair) scalar
+// multiplication, one lane per pair for the combine -- so this is plain VALU
+// integer work: no MFMA, no LDS.
+//
+// Field: p = 2^256 - 2^224 + 2^192 + 2^96 - 1, eight 32-bit limbs little
+// endian, Montgomery form with R = 2^256 (-p^-1 mod 2^32 = 1, so the CIOS
+// quotient digit is the low limb itself).  Points: Jacobian (X, Y, Z), Z = 0
+// is the point at infinity; curve a = -3.
+// Wire format (host <-> device): points are 64 bytes x||y, each a 32-byte
+// big-endian integer (SEC1 uncompressed without the 0x04 prefix; the same
+// bytes the reference hashes at :584-585); scalars are 32-byte big endian.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "flm_internal.h"
+
+namespace flm {
+namespace {
+
+struct Fe {
+    uint32_t v[8];
+};
+struct Jac {
+    Fe X, Y, Z;
+};
+
+__device__ constexpr uint32_t kP[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 1u, 0xffffffffu};
+__device__ constexpr uint32_t kOne[8] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu,
+                                         0xffffffffu, 0xffffffffu, 0xfffffffeu, 0x00000000u};  // R mod p
+__device__ constexpr uint32_t kR2[8] = {0x00000003u, 0x00000000u, 0xffffffffu, 0xfffffffbu,
+                                        0xfffffffeu, 0xffffffffu, 0xfffffffdu, 0x00000004u};  // R^2 mod p
+__device__ constexpr uint32_t kBm[8] = {0x29c4bddfu, 0xd89cdf62u, 0x78843090u, 0xacf005cdu,
+                                        0xf7212ed6u, 0xe5a220abu, 0x04874834u, 0xdc30061du};  // b*R mod p
+
+__device__ __forceinline__ Fe fe_const(const uint32_t (&c)[8]) {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = c[i];
+    return r;
+}
+
+__device__ __forceinline__ bool fe_is_zero(const Fe &a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.v[i];
+    return o == 0;
+}
+
+__device__ __forceinline__ bool fe_eq(const Fe &a, const Fe &b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.v[i] ^ b.v[i];
+    return o == 0;
+}
+
+// a < p for a canonical (non-Montgomery) input
+__device__ __forceinline__ bool fe_lt_p(const Fe &a) {
+    uint64_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t d = (uint64_t)a.v[i] - kP[i] - b;
+        b = d >> 63;
+    }
+    return b != 0;
+}
+
+// r = (t8:t) - p if that does not borrow (or t8 set), else t; requires t < 2p
+__device__ __forceinline__ void fe_reduce_once(Fe &r, const uint32_t (&t)[8], uint32_t t8) {
+    uint32_t d[8];
+    uint64_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t x = (uint64_t)t[i] - kP[i] - b;
+        d[i] = (uint32_t)x;
+        b = x >> 63;
+    }
+    bool take = t8 || !b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = take ? d[i] : t[i];
+}
+
+__device__ __forceinline__ Fe fe_add(const Fe &a, const Fe &b) {
+    uint32_t s[8];
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c = (uint64_t)a.v[i] + b.v[i] + (c >> 32);
+        s[i] = (uint32_t)c;
+    }
+    Fe r;
+    fe_reduce_once(r, s, (uint32_t)(c >> 32));
+    return r;
+}
+
+__device__ __forceinline__ Fe fe_sub(const Fe &a, const Fe &b) {
+    uint32_t d[8];
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t x = (uint64_t)a.v[i] - b.v[i] - br;
+        d[i] = (uint32_t)x;
+        br = x >> 63;
+    }
+    // borrow -> add p back (mask instead of branch)
+    uint32_t m = 0u - (uint32_t)br;
+    Fe r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c = (uint64_t)d[i] + (kP[i] & m) + (c >> 32);
+        r.v[i] = (uint32_t)c;
+    }
+    return r;
+}
+
+// Montgomery product a*b*R^-1 mod p (CIOS, quotient digit = low limb since -p^-1 = 1 mod 2^32)
+__device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
+    uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t t8 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c = (uint64_t)a.v[j] * b.v[i] + t[j] + (c >> 32);
+            t[j] = (uint32_t)c;
+        }
+        uint64_t s = (uint64_t)t8 + (c >> 32);
+        uint32_t hi0 = (uint32_t)s, hi1 = (uint32_t)(s >> 32);
+        uint32_t m = t[0];
+        // (t + m*p) / 2^32 with p's limbs {-1,-1,-1,0,0,0,1,-1}
+        c = (uint64_t)m * kP[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            c = (uint64_t)m * kP[j] + t[j] + (c >> 32);
+            t[j - 1] = (uint32_t)c;
+        }
+        s = (uint64_t)hi0 + (c >> 32);
+        t[7] = (uint32_t)s;
+        t8 = hi1 + (uint32_t)(s >> 32);
+    }
+    Fe r;
+    fe_reduce_once(r, t, t8);
+    return r;
+}
+
+__device__ __forceinline__ Fe fe_sqr(const Fe &a) { return fe_mul(a, a); }
+
+__device__ __forceinline__ Fe fe_neg(const Fe &a) {
+    Fe z = {};
+    return fe_sub(z, a);
+}
+
+__device__ __forceinline__ Fe to_mont(const Fe &a) { return fe_mul(a, fe_const(kR2)); }
+__device__ __forceinline__ Fe from_mont(const Fe &a) {
+    Fe one = {};
+    one.v[0] = 1;
+    return fe_mul(a, one);
+}
+
+// a^(p-2): p-2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
+__device__ Fe fe_inv(const Fe &a) {
+    // x_k = a^(2^k - 1)
+    Fe x2 = fe_mul(fe_sqr(a), a);
+    Fe x4 = x2;
+    for (int i = 0; i < 2; ++i) x4 = fe_sqr(x4);
+    x4 = fe_mul(x4, x2);
+    Fe x8 = x4;
+    for (int i = 0; i < 4; ++i) x8 = fe_sqr(x8);
+    x8 = fe_mul(x8, x4);
+    Fe x16 = x8;
+    for (int i = 0; i < 8; ++i) x16 = fe_sqr(x16);
+    x16 = fe_mul(x16, x8);
+    Fe x32 = x16;
+    for (int i = 0; i < 16; ++i) x32 = fe_sqr(x32);
+    x32 = fe_mul(x32, x16);
+    // top 32 bits ffffffff, then 00000001
+    Fe r = x32;
+    for (int i = 0; i < 32; ++i) r = fe_sqr(r);
+    r = fe_mul(r, a);                       // ...00000001
+    for (int i = 0; i < 128; ++i) r = fe_sqr(r);  // three zero words + one more shift below
+    r = fe_mul(r, x32);                     // ffffffff
+    for (int i = 0; i < 32; ++i) r = fe_sqr(r);
+    r = fe_mul(r, x32);                     // ffffffff
+    // last word fffffffd = 30 ones, 0, 1
+    for (int i = 0; i < 16; ++i) r = fe_sqr(r);
+    r = fe_mul(r, x16);
+    Fe x14 = x8;                            // 2^14 - 1 = x8 shifted 6 + x4 (2 bits) ... build 14 ones
+    for (int i = 0; i < 4; ++i) x14 = fe_sqr(x14);
+    x14 = fe_mul(x14, x4);                  // 12 ones
+    x14 = fe_sqr(fe_sqr(x14));
+    x14 = fe_mul(x14, x2);                  // 14 ones
+    for (int i = 0; i < 14; ++i) r = fe_sqr(r);
+    r = fe_mul(r, x14);                     // 30 ones
+    r = fe_sqr(r);                          // 0
+    r = fe_sqr(r);
+    r = fe_mul(r, a);                       // 1
+    return r;
+}
+
+// -------------------------------------------------------------- points (a = -3)
+__device__ __forceinline__ Jac jac_inf() {
+    Jac r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.X.v[i] = r.Y.v[i] = r.Z.v[i] = 0;
+    r.X = fe_const(kOne);
+    r.Y = fe_const(kOne);
+    return r;
+}
+
+// dbl-2001-b
+__device__ __forceinline__ Jac jac_dbl(const Jac &P) {
+    Fe delta = fe_sqr(P.Z);
+    Fe gamma = fe_sqr(P.Y);
+    Fe beta = fe_mul(P.X, gamma);
+    Fe t = fe_mul(fe_sub(P.X, delta), fe_add(P.X, delta));
+    Fe alpha = fe_add(fe_add(t, t), t);
+    Fe beta2 = fe_add(beta, beta);
+    Fe beta4 = fe_add(beta2, beta2);
+    Fe beta8 = fe_add(beta4, beta4);
+    Jac R;
+    R.X = fe_sub(fe_sqr(alpha), beta8);
+    Fe yz = fe_add(P.Y, P.Z);
+    R.Z = fe_sub(fe_sub(fe_sqr(yz), gamma), delta);
+    Fe g2 = fe_sqr(gamma);
+    Fe g4 = fe_add(g2, g2);
+    Fe g8 = fe_add(g4, g4);
+    g8 = fe_add(g8, g8);
+    R.Y = fe_sub(fe_mul(alpha, fe_sub(beta4, R.X)), g8);
+    return R;
+}
+
+// add-2007-bl with the exceptional cases (P == Q, P == -Q, infinity) handled
+__device__ Jac jac_add(const Jac &P, const Jac &Q) {
+    if (fe_is_zero(P.Z)) return Q;
+    if (fe_is_zero(Q.Z)) return P;
+    Fe z1z1 = fe_sqr(P.Z);
+    Fe z2z2 = fe_sqr(Q.Z);
+    Fe u1 = fe_mul(P.X, z2z2);
+    Fe u2 = fe_mul(Q.X, z1z1);
+    Fe s1 = fe_mul(fe_mul(P.Y, Q.Z), z2z2);
+    Fe s2 = fe_mul(fe_mul(Q.Y, P.Z), z1z1);
+    Fe h = fe_sub(u2, u1);
+    Fe r = fe_sub(s2, s1);
+    if (fe_is_zero(h)) {
+        if (fe_is_zero(r)) return jac_dbl(P);
+        return jac_inf();
+    }
+    r = fe_add(r, r);
+    Fe h2 = fe_add(h, h);
+    Fe i = fe_sqr(h2);
+    Fe j = fe_mul(h, i);
+    Fe v = fe_mul(u1, i);
+    Jac R;
+    R.X = fe_sub(fe_sub(fe_sqr(r), j), fe_add(v, v));
+    Fe s1j = fe_mul(s1, j);
+    R.Y = fe_sub(fe_mul(r, fe_sub(v, R.X)), fe_add(s1j, s1j));
+    Fe zz = fe_add(P.Z, Q.Z);
+    R.Z = fe_mul(fe_sub(fe_sub(fe_sqr(zz), z1z1), z2z2), h);
+    return R;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// 32-byte big endian -> limbs
+__device__ __forceinline__ Fe load_be(const uint8_t *p) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint4 a = q[0], b = q[1];
+    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    Fe r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.v[k] = bswap32(w[7 - k]);
+    return r;
+}
+
+__device__ __forceinline__ void store_be(uint8_t *p, const Fe &a) {
+    uint4 *q = reinterpret_cast<uint4 *>(p);
+    q[0] = make_uint4(bswap32(a.v[7]), bswap32(a.v[6]), bswap32(a.v[5]), bswap32(a.v[4]));
+    q[1] = make_uint4(bswap32(a.v[3]), bswap32(a.v[2]), bswap32(a.v[1]), bswap32(a.v[0]));
+}
+
+// Load an affine wire point; false if a coordinate is >= p or the point is off the curve.
+__device__ __forceinline__ bool load_point(const uint8_t *p, Jac &out) {
+    Fe x = load_be(p), y = load_be(p + 32);
+    bool ok = fe_lt_p(x) && fe_lt_p(y);
+    x = to_mont(x);
+    y = to_mont(y);
+    // y^2 == x^3 - 3x + b
+    Fe rhs = fe_mul(fe_sqr(x), x);
+    Fe x3 = fe_add(fe_add(x, x), x);
+    rhs = fe_add(fe_sub(rhs, x3), fe_const(kBm));
+    ok = ok && fe_eq(fe_sqr(y), rhs);
+    out.X = x;
+    out.Y = y;
+    out.Z = fe_const(kOne);
+    return ok;
+}
+
+// ------------------------------------------------------------------ SHA-256
+__device__ constexpr uint32_t kK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+__device__ void sha256_block(uint32_t (&h)[8], const uint32_t (&m)[16]) {
+    uint32_t w[64];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = m[t];
+#pragma unroll
+    for (int t = 16; t < 64; ++t) {
+        uint32_t s0 = rotr(w[t - 15], 7) ^ rotr(w[t - 15], 18) ^ (w[t - 15] >> 3);
+        uint32_t s1 = rotr(w[t - 2], 17) ^ rotr(w[t - 2], 19) ^ (w[t - 2] >> 10);
+        w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = hh + S1 + ch + kK[t] + w[t];
+        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        uint32_t t2 = S0 + mj;
+        hh = g;
+        g = f;
+        f = e;
+        e = d + t1;
+        d = c;
+        c = b;
+        b = a;
+        a = t1 + t2;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+    h[5] += f;
+    h[6] += g;
+    h[7] += hh;
+}
+
+// SHA-256 of the 64-byte big-endian x||y; digest written as 32 bytes
+__device__ void sha256_point(const Fe &x, const Fe &y, uint8_t *out) {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint32_t m[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        m[t] = x.v[7 - t];
+        m[8 + t] = y.v[7 - t];
+    }
+    sha256_block(h, m);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) m[t] = 0;
+    m[0] = 0x80000000u;
+    m[15] = 512;
+    sha256_block(h, m);
+    uint4 *q = reinterpret_cast<uint4 *>(out);
+    q[0] = make_uint4(bswap32(h[0]), bswap32(h[1]), bswap32(h[2]), bswap32(h[3]));
+    q[1] = make_uint4(bswap32(h[4]), bswap32(h[5]), bswap32(h[6]), bswap32(h[7]));
+}
+
+// ------------------------------------------------------------------ kernels
+constexpr int kEcThreads = 64;
+
+__device__ __forceinline__ void store_jac(uint32_t *jac, size_t plane_stride, const Jac &R) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        jac[(size_t)k * plane_stride] = R.X.v[k];
+        jac[(size_t)(8 + k) * plane_stride] = R.Y.v[k];
+        jac[(size_t)(16 + k) * plane_stride] = R.Z.v[k];
+    }
+}
+
+__device__ __forceinline__ Jac load_jac(const uint32_t *jac, size_t plane_stride) {
+    Jac R;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        R.X.v[k] = jac[(size_t)k * plane_stride];
+        R.Y.v[k] = jac[(size_t)(8 + k) * plane_stride];
+        R.Z.v[k] = jac[(size_t)(16 + k) * plane_stride];
+    }
+    return R;
+}
+
+// Scalar multiplication scalar * point for T x D (term, element) pairs.
+// points: [T][D][64] wire bytes; scalars: [T][32] (one per term, uniform over a
+// workgroup) or [T][D][32] when per_element; jac out: SoA planes [T][24][D].
+// Fixed 4-bit windows from the most significant nibble; 4 doublings + 1 add per window.
+__global__ __launch_bounds__(kEcThreads) void ec_mul_kernel(const uint8_t *__restrict__ points,
+                                                            const uint8_t *__restrict__ scalars, int per_element,
+                                                            int D, uint32_t *__restrict__ jac,
+                                                            uint32_t *__restrict__ flags) {
+    const int j = blockIdx.y;
+    const int i = blockIdx.x * kEcThreads + threadIdx.x;
+    if (i >= D) return;
+    const size_t e = (size_t)j * D + i;
+    Jac P;
+    bool ok = load_point(points + e * 64, P);
+    if (!ok) atomicOr(&flags[i], 2u);
+    const uint8_t *k = scalars + (per_element ? e : (size_t)j) * 32;
+
+    Jac tab[16];
+    tab[0] = jac_inf();
+    tab[1] = P;
+    tab[2] = jac_dbl(P);
+#pragma unroll 1
+    for (int t = 3; t < 16; ++t) tab[t] = jac_add(tab[t - 1], P);
+
+    Jac acc = tab[k[0] >> 4];
+#pragma unroll 1
+    for (int w = 1; w < 64; ++w) {
+        if (!fe_is_zero(acc.Z)) {
+            acc = jac_dbl(acc);
+            acc = jac_dbl(acc);
+            acc = jac_dbl(acc);
+            acc = jac_dbl(acc);
+        }
+        uint32_t byte = k[w >> 1];
+        uint32_t d = (w & 1) ? (byte & 15u) : (byte >> 4);
+        if (d) acc = jac_add(acc, tab[d]);
+    }
+    if (!ok) acc = jac_inf();
+    store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
+}
+
+// Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
+// write the affine wire point and optionally SHA-256(x||y).
+// flags bit 0: base off-curve, bit 1: an input share was off-curve (ec_mul), bit 2: result at infinity.
+__global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__restrict__ base,
+                                                               const uint32_t *__restrict__ jac, int T, int D,
+                                                               int negate, uint8_t *__restrict__ points_out,
+                                                               uint8_t *__restrict__ digests_out,
+                                                               uint32_t *__restrict__ flags) {
+    const int i = blockIdx.x * kEcThreads + threadIdx.x;
+    if (i >= D) return;
+    uint32_t fl = 0;
+    Jac acc = jac_inf();
+    if (base) {
+        if (!load_point(base + (size_t)i * 64, acc)) {
+            fl |= 1u;
+            acc = jac_inf();
+        }
+    }
+#pragma unroll 1
+    for (int j = 0; j < T; ++j) {
+        Jac R = load_jac(jac + (size_t)j * 24 * D + i, (size_t)D);
+        if (negate) R.Y = fe_neg(R.Y);
+        acc = jac_add(acc, R);
+    }
+    Fe x = {}, y = {};
+    if (fe_is_zero(acc.Z)) {
+        fl |= 4u;
+    } else {
+        Fe zi = fe_inv(acc.Z);
+        Fe zi2 = fe_sqr(zi);
+        x = from_mont(fe_mul(acc.X, zi2));
+        y = from_mont(fe_mul(acc.Y, fe_mul(zi2, zi)));
+    }
+    if (points_out) {
+        store_be(points_out + (size_t)i * 64, x);
+        store_be(points_out + (size_t)i * 64 + 32, y);
+    }
+    if (digests_out) sha256_point(x, y, digests_out + (size_t)i * 32);
+    if (fl) atomicOr(&flags[i], fl);
+}
+
+}  // namespace
+
+hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream) {
+    if (T <= 0 || D <= 0) return hipSuccess;
+    dim3 grid((D + kEcThreads - 1) / kEcThreads, T);
+    hipLaunchKernelGGL(ec_mul_kernel, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, per_element, D, d_jac,
+                       d_flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T, int D, int negate,
+                            uint8_t *d_points_out, uint8_t *d_digests_out, uint32_t *d_flags, hipStream_t stream) {
+    if (D <= 0) return hipSuccess;
+    dim3 grid((D + kEcThreads - 1) / kEcThreads);
+    hipLaunchKernelGGL(ec_finish_kernel, grid, dim3(kEcThreads), 0, stream, d_base, d_jac, T, D, negate,
+                       d_points_out, d_digests_out, d_flags);
+    return hipGetLastError();
+}
+
+}  // namespace flm

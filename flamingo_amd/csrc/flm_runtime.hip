@@ -80,6 +80,7 @@ struct flm_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out;
+    DevBuf ec_in, ec_base, ec_scal, ec_jac, ec_out, ec_dig, ec_flags;  // P-256 batches
     // pinned staging ring for pageable host rows: two buffers, each reused once
     // the DMA that read it has completed (event per buffer)
     void *stage[2] = {nullptr, nullptr};
@@ -540,7 +541,8 @@ void flm_free(flm_ctx *ctx) {
     }
     ctx->scratch_plan.items.release();
     for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
-                      &ctx->bytes_out})
+                      &ctx->bytes_out, &ctx->ec_in, &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out,
+                      &ctx->ec_dig, &ctx->ec_flags})
         b->release();
     for (int i = 0; i < 2; ++i) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
@@ -821,6 +823,96 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
     if (tile_slots) *tile_slots = ctx->last_tile;
     if (atomics) *atomics = ctx->last_atomics;
     if (variant) *variant = ctx->last_variant;
+    return 0;
+}
+
+// ------------------------------------------------------------------ P-256
+static int ec_dims(flm_ctx *ctx, int T, int D) {
+    if (T < 0 || D < 0) return fail(ctx, FLM_EINVAL, "negative batch size (T=%d, D=%d)", T, D);
+    if ((size_t)T * (size_t)D > (size_t)1 << 26) return fail(ctx, FLM_EINVAL, "batch too large (T*D=%zu)", (size_t)T * D);
+    return 0;
+}
+
+int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_shares, const uint8_t *d_lambdas, int T,
+                       int D, int negate, uint8_t *d_points_out, uint8_t *d_seeds_out, uint32_t *d_flags,
+                       void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, T, D)) return rc;
+    if (D == 0) return 0;
+    if ((T > 0 && (!d_shares || !d_lambdas)) || !d_flags) return fail(ctx, FLM_EINVAL, "NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
+    FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
+    FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s));
+    FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), T, D, negate, d_points_out, d_seeds_out,
+                                       d_flags, s));
+    return 0;
+}
+
+int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const uint8_t *lambdas, int T, int D,
+                   int negate, uint8_t *points_out, uint8_t *seeds_out, uint32_t *flags_out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, T, D)) return rc;
+    if (D == 0) return 0;
+    if (T > 0 && (!shares || !lambdas)) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t nsh = (size_t)T * D * 64;
+    FLM_HIP(ctx, ctx->ec_in.reserve(nsh));
+    FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)T * 32));
+    FLM_HIP(ctx, ctx->ec_base.reserve((size_t)D * 64));
+    FLM_HIP(ctx, ctx->ec_out.reserve((size_t)D * 64));
+    FLM_HIP(ctx, ctx->ec_dig.reserve((size_t)D * 32));
+    FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)D * 4));
+    hipStream_t s = ctx->stream;
+    if (T > 0) {
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, shares, nsh, hipMemcpyHostToDevice, s));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lambdas, (size_t)T * 32, hipMemcpyHostToDevice, s));
+    }
+    if (c1) FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_base.p, c1, (size_t)D * 64, hipMemcpyHostToDevice, s));
+    if (int rc = flm_ec_combine_dev(ctx, c1 ? ctx->ec_base.as<uint8_t>() : nullptr, ctx->ec_in.as<uint8_t>(),
+                                    ctx->ec_scal.as<uint8_t>(), T, D, negate, ctx->ec_out.as<uint8_t>(),
+                                    ctx->ec_dig.as<uint8_t>(), ctx->ec_flags.as<uint32_t>(), s))
+        return rc;
+    std::vector<uint32_t> fl(D);
+    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)D * 4, hipMemcpyDeviceToHost, s));
+    if (points_out) FLM_HIP(ctx, hipMemcpyAsync(points_out, ctx->ec_out.p, (size_t)D * 64, hipMemcpyDeviceToHost, s));
+    if (seeds_out) FLM_HIP(ctx, hipMemcpyAsync(seeds_out, ctx->ec_dig.p, (size_t)D * 32, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
+    for (int i = 0; i < D; ++i)
+        if (fl[i] & 3u)
+            return fail(ctx, FLM_EINVAL, "element %d: %s is not a point on P-256", i,
+                        (fl[i] & 1u) ? "ciphertext c1" : "a decryption share");
+    return 0;
+}
+
+int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, 1, n)) return rc;
+    if (n == 0) return 0;
+    if (!points || !scalars || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_HIP(ctx, ctx->ec_in.reserve((size_t)n * 64));
+    FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)n * 32));
+    FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)n * 96));
+    FLM_HIP(ctx, ctx->ec_out.reserve((size_t)n * 64));
+    FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)n * 4));
+    hipStream_t s = ctx->stream;
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, points, (size_t)n * 64, hipMemcpyHostToDevice, s));
+    FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, scalars, (size_t)n * 32, hipMemcpyHostToDevice, s));
+    FLM_HIP(ctx, hipMemsetAsync(ctx->ec_flags.p, 0, (size_t)n * 4, s));
+    FLM_HIP(ctx, flm::launch_ec_mul(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), 1, 1, n,
+                                    ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s));
+    FLM_HIP(ctx, flm::launch_ec_finish(nullptr, ctx->ec_jac.as<uint32_t>(), 1, n, 0, ctx->ec_out.as<uint8_t>(),
+                                       nullptr, ctx->ec_flags.as<uint32_t>(), s));
+    std::vector<uint32_t> fl(n);
+    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->ec_out.p, (size_t)n * 64, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
+    for (int i = 0; i < n; ++i)
+        if (fl[i] & 2u) return fail(ctx, FLM_EINVAL, "element %d: input is not a point on P-256", i);
     return 0;
 }
 

@@ -248,6 +248,60 @@ class MaskEngine:
         self._check(rc, "flm_prg_expand_dev")
         return out
 
+    # ------------------------------------------------------------ P-256
+    def ec_mul(self, points, scalars) -> list:
+        """[k_i * P_i] for affine points (x, y) and integer scalars (flm_ec_mul).
+
+        The ECDH / ElGamal / decryption-share products of SA_ClientAgent.py:256-263,
+        :434-447 and :397-400, batched.  Infinity comes back as None."""
+        from .crypto import points_from_wire, points_to_wire, scalars_to_wire
+        n = len(points)
+        if len(scalars) != n:
+            raise RuntimeError(f"{len(scalars)} scalars for {n} points")
+        if n == 0:
+            return []
+        pw, sw = points_to_wire(points), scalars_to_wire(scalars)
+        out = np.zeros((n, 64), np.uint8)
+        fl = np.zeros(n, np.uint32)
+        self._check(self.lib.flm_ec_mul(self.ctx, p_u8(pw), p_u8(sw), n, p_u8(out), p_u32(fl)), "flm_ec_mul")
+        return points_from_wire(out, fl)
+
+    def ec_combine(self, c1, shares_by_term, lambdas, negate: bool = True):
+        """Threshold-ElGamal combine + seed derivation (SA_ServiceAgent.py:542-585).
+
+        c1: D affine points (or None: base = infinity); shares_by_term: T lists of D
+        points (share_{j,i} = sk_j * c0_i); lambdas: T Lagrange coefficients.
+        Returns (points, seeds): point_i = c1_i - sum_j lambda_j share_{j,i}
+        (+ when negate is False) and seed_i = SHA-256(x||y) as 32 bytes."""
+        from .crypto import points_from_wire, points_to_wire, scalars_to_wire
+        T = len(lambdas)
+        D = len(c1) if c1 is not None else (len(shares_by_term[0]) if T else 0)
+        if len(shares_by_term) != T or any(len(s) != D for s in shares_by_term):
+            raise RuntimeError("shares must be T lists of D points")
+        if D == 0:
+            return [], []
+        sh = np.concatenate([points_to_wire(s) for s in shares_by_term]) if T else np.zeros((1, 64), np.uint8)
+        lw = scalars_to_wire(lambdas) if T else np.zeros((1, 32), np.uint8)
+        cw = points_to_wire(c1) if c1 is not None else None
+        pts = np.zeros((D, 64), np.uint8)
+        seeds = np.zeros((D, 32), np.uint8)
+        fl = np.zeros(D, np.uint32)
+        rc = self.lib.flm_ec_combine(self.ctx, p_u8(cw) if cw is not None else None, p_u8(sh), p_u8(lw), T, D,
+                                     1 if negate else 0, p_u8(pts), p_u8(seeds), p_u32(fl))
+        self._check(rc, "flm_ec_combine")
+        return points_from_wire(pts, fl), [bytes(r) for r in seeds]
+
+    def ec_combine_dev(self, c1, shares, lambdas, seeds_out, flags, points_out=None, negate: bool = True,
+                       stream=None):
+        """Device form: c1 (D,64), shares (T,D,64), lambdas (T,32) uint8 CUDA tensors;
+        seeds_out (D,32) uint8 and flags (D,) int32 CUDA tensors are written on `stream`."""
+        T, D = shares.shape[0], shares.shape[1]
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+        rc = self.lib.flm_ec_combine_dev(self.ctx, vp(c1), vp(shares), vp(lambdas), T, D, 1 if negate else 0,
+                                         vp(points_out), vp(seeds_out), vp(flags), self._stream_handle(stream))
+        self._check(rc, "flm_ec_combine_dev")
+        return seeds_out
+
     def check_signs(self) -> int:
         bad = ctypes.c_int()
         self._check(self.lib.flm_check_signs(self.ctx, ctypes.byref(bad)), "flm_check_signs")

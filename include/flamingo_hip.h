@@ -157,6 +157,38 @@ int flm_plan_aggregate(int subtiles, int pairing, size_t row_pitch, int N, int K
                        size_t mask_hi, uint64_t prg_slot0, void *items_out, int max_items, int *n_items,
                        int *plan_flags);
 
+/* ------------------------------------------------------- P-256 seed recovery */
+
+/* Wire format: a point is 64 bytes x||y, each coordinate a 32-byte big-endian
+ * integer < p (what the reference hashes, SA_ServiceAgent.py:583-585); a
+ * scalar is 32 bytes big endian.  The point at infinity is returned as 64 zero
+ * bytes (pycryptodome's EccPoint(0, 0)); flags bit 2 marks it.
+ *
+ * Threshold-ElGamal combine + key derivation, replacing
+ * SA_ServiceAgent.reconstruction_process's pairwise branch (:542-585):
+ *   point_i = c1_i + (negate ? -1 : +1) * sum_{j<T} lambdas[j] * shares[j][i]
+ *   seed_i  = SHA-256(point_i wire bytes)          (the 32-byte ChaCha20 key)
+ * for i < D, where shares[j][i] = sk_j * c0_i is committee member j's
+ * decryption share (SA_ClientAgent.py:397-400) and lambdas are the Lagrange
+ * coefficients at 0 (util/crypto/secretsharing points_to_secret_int).  The
+ * reference computes -(sum) + c1 (negate = 1).  c1 may be NULL (base = point
+ * at infinity).  shares: T*D*64 bytes, term-major; lambdas: T*32 bytes.
+ * points_out (D*64), seeds_out (D*32) and flags_out (D) may each be NULL.
+ * Returns FLM_EINVAL if any input point is not on P-256 (flags bit 0 = c1,
+ * bit 1 = a share), as pycryptodome's EccPoint constructor raises. */
+int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const uint8_t *lambdas, int T, int D,
+                   int negate, uint8_t *points_out, uint8_t *seeds_out, uint32_t *flags_out);
+/* Device-pointer form (enqueued on `stream`; flags are written, not checked).
+ * The seeds can feed flm_seed_table_dev directly, so seed recovery and the
+ * unmask run back to back without a host round trip. */
+int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_shares, const uint8_t *d_lambdas, int T,
+                       int D, int negate, uint8_t *d_points_out, uint8_t *d_seeds_out, uint32_t *d_flags,
+                       void *stream);
+/* Batched scalar multiplication out[i] = scalars[i] * points[i]: the ECDH
+ * (SA_ClientAgent.py:256-263), ElGamal (:434-447) and decryption-share
+ * (:397-400) products, n independent elements per call. */
+int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out);
+
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */
 void *flm_host_alloc(size_t bytes);
