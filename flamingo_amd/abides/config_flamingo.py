@@ -45,6 +45,7 @@ def parse(argv):
     ap.add_argument("--vector_len", type=int, default=P.vector_len)
     ap.add_argument("--root_seed_hex", default=None)
     ap.add_argument("--offline", default="")
+    ap.add_argument("--committee_size", type=int, default=P.committee_size)
     args, _ = ap.parse_known_args(argv)
     return ap, args
 
@@ -61,7 +62,9 @@ def run(argv=None):
     if not P.assert_power_of_two(n):
         raise ValueError("Number of clients must be power of 2")
     root = bytes.fromhex(args.root_seed_hex) if args.root_seed_hex else None
-    param.configure(root=root, L=args.vector_len)
+    if args.committee_size > args.num_clients:
+        raise ValueError("committee_size cannot exceed num_clients")
+    param.configure(root=root, L=args.vector_len, committee=args.committee_size)
     offline = {int(x) for x in args.offline.split(",") if x.strip()}
     print(f"Silent mode: {log.silent_mode}")
     print(f"Configuration seed: {seed}\n")

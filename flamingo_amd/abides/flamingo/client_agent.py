@@ -1,30 +1,39 @@
 """Flamingo client agent (agent/flamingo/SA_ClientAgent.py surface).
 
 Per iteration the client (sendVectors, :198-348) finds its neighbours, draws
-its self-mask seed m_i, deals Shamir shares of m_i to the committee, derives a
-pairwise seed per neighbour and sends the masked vector
+its self-mask seed m_i, Shamir-shares it to the committee (each share AES-GCM
+encrypted under the ECDH key with that member, :214-244), derives a pairwise
+seed per neighbour -- ECDH r_ij = a_i A_j -> SHA-256 -> key; h_ijt =
+ChaCha20(key)(t) & 0xFFFF; H = hash_to_curve(h_ijt); s_ij = SHA-256(H)
+(:253-292) -- ElGamal-encrypts H under the system key (:326-332, :434-447)
+and sends the masked vector
 
     y_i = x_i + PRG(m_i) + sum_{j in N(i), j > i} PRG(s_ij) - sum_{j < i} PRG(s_ij)
 
-(:304-324; x_i = all ones, :304).  The mask expansion and composition run on
-the GPU (MaskEngine.client_mask).  Committee members answer the server's SIGN
-and DEC requests (signSendLabels :351-368, decryptSendShares :370-431).
-Crypto stand-ins: see seeds.py.
+(:304-324; x_i = all ones, :304).  GPU work: the mask expansion and
+composition (MaskEngine.client_mask) and every batch of P-256 scalar
+multiplications (ECDH, ElGamal, decryption shares: MaskEngine.ec_mul_wire).
+Committee members sign the offline set (ECDSA, :351-368) and answer DEC with
+sk_j * c0 for each dropout ciphertext plus their decrypted m_i shares
+(:370-431).
 """
 from __future__ import annotations
 
 import hashlib
-import json
 import logging
 
 import numpy as np
 import pandas as pd
 
+from ... import crypto as C
 from ..agent import Agent
 from ..message import Message
 from . import protocol as param
-from .seeds import P256_N, pair_seed, shamir_share
+from . import wire
+from .seeds import P256_N, shamir_share
 from .service_agent import SA_ServiceAgent as ServiceAgent
+
+_MASK128 = (1 << 128) - 1
 
 
 class SA_ClientAgent(Agent):
@@ -59,6 +68,16 @@ class SA_ClientAgent(Agent):
         # in the reference dropouts only come from late messages)
         self.offline_iterations = set(offline_iterations)
         self.input_vector = None     # None -> all ones (:304)
+        pki = param.pki(num_clients)
+        self.secret_key = pki.client_sk[id]
+        self.public_key = pki.client_pk[id]
+        self.system_pk = pki.system_pk
+        self.pair_keys = {}          # neighbour -> SHA-256(a_i A_j)[:32]   (:256-263), cached across iterations
+        self.committee_keys = {}     # member -> AES key (a_i A_c).x mod 2^128 (:234-236)
+        self.symmetric_keys = {}     # (committee members) client -> AES key (:86-91)
+        if id in self.user_committee:
+            ids = list(range(num_clients))
+            self.symmetric_keys = self._aes_keys(ids)
 
     def kernelStarting(self, startTime):
         if self.id == 0:
@@ -96,8 +115,7 @@ class SA_ClientAgent(Agent):
                 t0 = pd.Timestamp("now")
                 if self.cipher_stored is not None and self.cipher_stored.body["iteration"] == self.current_iteration:
                     b = self.cipher_stored.body
-                    self.decryptSendShares(json.loads(b["dec_target_pairwise"]), json.loads(b["dec_target_mi"]),
-                                           b["client_id_list"])
+                    self.decryptSendShares(b["dec_target_pairwise"], b["dec_target_mi"], b["client_id_list"])
                 self.cipher_stored = None
                 self.recordTime(t0, "RECONSTRUCTION")
         elif body["msg"] == "REQ" and self.current_iteration != 0:
@@ -109,53 +127,104 @@ class SA_ClientAgent(Agent):
             self.recordTime(t0, "REPORT")
 
     # --------------------------------------------------------------- round
+    def _ecdh(self, ids) -> np.ndarray:
+        """a_i * A_j for the given clients, one GPU batch; (len, 64) wire rows."""
+        ids = list(ids)
+        pki = param.pki(self.num_clients)
+        out, _ = param.engine().ec_mul_wire(pki.pk_wire(ids), C.scalars_to_wire([self.secret_key] * len(ids)))
+        return out
+
+    def _aes_keys(self, ids) -> dict:
+        w = self._ecdh(ids)
+        return {j: (int.from_bytes(bytes(w[k, :32]), "big") & _MASK128).to_bytes(16, "big")
+                for k, j in enumerate(ids)}
+
+    def _rand_scalar(self) -> int:
+        return int.from_bytes(bytes(self.random_state.randint(0, 256, size=32, dtype=np.uint8)), "big") % P256_N
+
     def sendVectors(self, currentTime):
         if self.current_iteration in self.offline_iterations:
             self.logger.info(f"client {self.id} is offline in iteration {self.current_iteration}")
             return
         self.neighbors_list = param.find_neighbors(param.root_seed, self.current_iteration, self.num_clients,
                                                    self.id, self.neighborhood_size)
+        nb = sorted(self.neighbors_list)
+        if self.id in self.neighbors_list:
+            raise RuntimeError("id itself appears in its neighbor list")
+        committee = sorted(self.user_committee)
+        # ECDH keys (cached: keys do not change between iterations)
+        missing = [j for j in nb if j not in self.pair_keys]
+        if missing:
+            w = self._ecdh(missing)
+            for k, j in enumerate(missing):
+                self.pair_keys[j] = hashlib.sha256(bytes(w[k])).digest()[: self.key_length]
+        if not self.committee_keys:
+            self.committee_keys = self._aes_keys(committee)
+
+        # m_i, its Shamir shares, one AES-GCM ciphertext per committee member (:214-244)
         mi_bytes = bytes(self.random_state.randint(0, 256, size=self.key_length, dtype=np.uint8))
         mi_number = int.from_bytes(mi_bytes, "big")
         threshold = int(param.fraction * len(self.user_committee))
-        shares = shamir_share(mi_number, max(1, threshold), len(self.user_committee), self.prime,
+        shares = shamir_share(mi_number, max(1, threshold), len(committee), self.prime,
                               rng=_PyRandom(self.random_state))
-        enc_mi_shares = [y for _, y in shares]           # AES-GCM stand-in: share values in the clear
-        seeds = [mi_bytes]
-        signs = [1]
-        pairwise = {}
-        for j in sorted(self.neighbors_list):
-            if j == self.id:
-                raise RuntimeError("id itself appears in its neighbor list")
-            s = pair_seed(param.root_seed, self.current_iteration, self.id, j)
-            seeds.append(s)
+        enc_mi_shares = []
+        for (_, y), cid in zip(shares, committee):
+            nonce = bytes(self.random_state.randint(0, 256, size=16, dtype=np.uint8))
+            ct, _ = C.aes_gcm_encrypt(self.committee_keys[cid], y.to_bytes(self.key_length, "big"), nonce)
+            enc_mi_shares.append((ct, nonce))
+
+        # pairwise seeds: h_ijt -> H (group element) -> s_ij (:266-292)
+        rnd = self.current_iteration.to_bytes(16, "big")
+        H, seeds, signs = {}, [mi_bytes], [1]
+        for j in nb:
+            h = C.chacha20_encrypt(self.pair_keys[j], rnd, param.nonce)
+            H[j] = param.hash_to_curve(str(int.from_bytes(h[:4], "big") & 0xFFFF))
+            seeds.append(hashlib.sha256(C.point_bytes(H[j])).digest()[: self.key_length])
             signs.append(1 if self.id < j else -1)
-            pairwise[json.dumps([self.id, j])] = s.hex()   # ElGamal stand-in
+
+        # ElGamal under the system key: c0 = rG, c1 = H + r pk (:434-447), one GPU batch
+        rs = [self._rand_scalar() for _ in nb]
+        base = np.concatenate([np.tile(np.frombuffer(C.point_bytes(C.G), np.uint8), (len(nb), 1)),
+                               np.tile(np.frombuffer(C.point_bytes(self.system_pk), np.uint8), (len(nb), 1))])
+        out, _ = param.engine().ec_mul_wire(base, C.scalars_to_wire(rs + rs))
+        pts = C.points_from_wire(out)
+        cipher = {(self.id, j): (pts[k], C.add(H[j], pts[len(nb) + k])) for k, j in enumerate(nb)}
+
         x = None if self.input_vector is None else np.asarray(self.input_vector, np.uint32)[None, :]
         vec = param.engine().client_mask(np.array([0, len(seeds)], np.int64), seeds, signs, self.vector_len, x=x)[0]
         self.sendMessage(self.serviceAgentID, Message({
             "msg": "VECTOR", "iteration": self.current_iteration, "sender": self.id, "vector": vec,
-            "enc_mi_shares": json.dumps(enc_mi_shares), "enc_pairwise": json.dumps(pairwise)}),
+            "enc_mi_shares": wire.serialize_tuples_bytes(enc_mi_shares),
+            "enc_pairwise": wire.serialize_dim1_elgamal(cipher)}),
             tag="comm_key_generation")
 
     def signSendLabels(self, currentTime, msg_to_sign):
-        labels, _ = msg_to_sign
-        sig = hashlib.sha256(b"%d" % self.id + labels.encode()).hexdigest()   # DSS stand-in
+        payload = repr(msg_to_sign).encode()          # the reference signs dill.dumps(msg) (:352-356)
+        sig = C.ecdsa_sign(self.secret_key, self.public_key, payload)
         self.sendMessage(self.serviceAgentID, Message({
             "msg": "SIGN", "iteration": self.current_iteration, "sender": self.id,
-            "signed_labels": (labels, sig), "committee_member_idx": self.committee_member_idx}),
+            "signed_labels": (payload, sig), "committee_member_idx": self.committee_member_idx}),
             tag="comm_sign_client")
 
     def decryptSendShares(self, dec_target_pairwise, dec_target_mi, client_id_list):
+        """dec_target_pairwise: serialize_dim1_elgamal JSON; dec_target_mi: serialize_tuples_bytes JSON."""
         if self.committee_shared_sk is None:
             self.sendMessage(self.serviceAgentID, Message({
                 "msg": "NO_SK_SHARE", "iteration": self.current_iteration, "sender": self.id,
                 "shared_result": None, "committee_member_idx": None}), tag="no_sk_share")
             return
+        # sk_j * c0 for every dropout ciphertext (:393-400), one GPU batch
+        _, c0w, _ = wire.elgamal_json_to_wire(dec_target_pairwise)
+        sk = self.committee_shared_sk[1]
+        dec_w, _ = param.engine().ec_mul_wire(c0w, C.scalars_to_wire([sk] * c0w.shape[0]))
+        # decrypt this member's m_i shares (:402-420)
+        dec_mi = []
+        for cid, (ct, nonce) in zip(client_id_list, wire.deserialize_tuples_bytes(dec_target_mi)):
+            dec_mi.append(int.from_bytes(C.aes_gcm_decrypt(self.symmetric_keys[cid], ct, nonce), "big"))
         self.sendMessage(self.serviceAgentID, Message({
             "msg": "SHARED_RESULT", "iteration": self.current_iteration, "sender": self.id,
-            "shared_result_pairwise": json.dumps(dec_target_pairwise),
-            "shared_result_mi": json.dumps(dec_target_mi),
+            "shared_result_pairwise": wire.wire_to_ecp_json(dec_w),
+            "shared_result_mi": wire.serialize_dim1_list(dec_mi),
             "committee_member_idx": self.committee_member_idx}), tag="comm_secret_sharing")
 
     def recordTime(self, startTime, categoryName):

@@ -22,6 +22,8 @@ nonce = P.nonce
 _engine = None
 _graphs: dict = {}
 _committees: dict = {}
+_pkis: dict = {}
+_h2c: dict = {}
 
 
 def configure(root: bytes | None = None, L: int | None = None, committee: int | None = None):
@@ -37,6 +39,7 @@ def configure(root: bytes | None = None, L: int | None = None, committee: int | 
         committee_size = int(committee)
     _graphs.clear()
     _committees.clear()
+    _pkis.clear()
 
 
 def engine():
@@ -71,3 +74,23 @@ def find_neighbors(root, current_iteration, num_clients, id, neighborhood_size) 
         return P.find_neighbors(root, current_iteration, num_clients, id, neighborhood_size,
                                 encrypt=engine().chacha20_encrypt)
     return neighbors(current_iteration, num_clients, neighborhood_size)[id]
+
+
+def pki(num_clients: int):
+    """Key material for this simulation (pki_files/ stand-in, see pki.py)."""
+    key = (root_seed, num_clients)
+    if key not in _pkis:
+        from .pki import PKI
+        _pkis.clear()
+        _pkis[key] = PKI(root_seed, num_clients, engine())
+    return _pkis[key]
+
+
+def hash_to_curve(h_ijt: str):
+    """ecchash.hash_str_to_curve(h_ijt, 2, n, m, L, XMD-SHA256) as the client calls it
+    (SA_ClientAgent.py:283-286).  h_ijt is a decimal string below 2^16, so results are memoised."""
+    pt = _h2c.get(h_ijt)
+    if pt is None:
+        from ...crypto import hash_str_to_curve
+        pt = _h2c[h_ijt] = hash_str_to_curve(h_ijt)
+    return pt

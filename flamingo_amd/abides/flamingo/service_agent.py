@@ -8,25 +8,28 @@ Four-step round state machine, same as the reference (:123-135):
 
 The hot loops are replaced by calls into the MI355X engine:
   report_process        S = sum_{i in U} y_i         (:346-350)  -> MaskEngine.aggregate_unmask(rows, K=0)
-  reconstruction_process out = S - sum PRG(m_i) + sum sigma PRG(s_ij)
-                        (:529-540, :587-605)          -> MaskEngine.mask_accumulate(seeds, signs, S)
-Both are bit-exact with the reference's numpy uint32 arithmetic.  Seed
-transport (Shamir real, encryption stand-in) is described in seeds.py.
+  reconstruction_process
+      s_ij for dropout pairs: c1 - sum_j lambda_j (sk_j c0), SHA-256   (:542-585) -> MaskEngine.ec_combine_wire
+      out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> MaskEngine.mask_accumulate
+The vector arithmetic is bit-exact with the reference's numpy uint32 code; m_i
+recovery (Lagrange at 0 over n, :506-526) stays on the host (T x |U| 256-bit
+products).  Message payloads use the reference's JSON formats (wire.py).
 """
 from __future__ import annotations
 
-import hashlib
 import json
 import logging
 
 import numpy as np
 import pandas as pd
 
+from ... import crypto as C
+from ... import params as P
 from ..agent import Agent
 from ..message import Message
 from . import protocol as param
+from . import wire
 from .seeds import P256_N, lagrange_at_zero, shamir_share
-from ... import params as P
 
 
 class SA_ServiceAgent(Agent):
@@ -100,9 +103,8 @@ class SA_ServiceAgent(Agent):
                 self.logger.info(f"LATE MSG: VECTOR from iteration {body['iteration']} client {sender}")
                 return
             self.recv_user_vectors[sender] = body["vector"]
-            self.recv_mi_cipher[sender] = json.loads(body["enc_mi_shares"])
-            for k, v in json.loads(body["enc_pairwise"]).items():
-                self.recv_pairwise_cipher[tuple(json.loads(k))] = v
+            self.recv_mi_cipher[sender] = wire.deserialize_tuples_bytes(body["enc_mi_shares"])
+            self.recv_pairwise_cipher.update(wire.deserialize_dim1_elgamal(body["enc_pairwise"]))
         elif body["msg"] == "SIGN":
             if not late:
                 self.recv_committee_sigs[sender] = body["signed_labels"]
@@ -110,8 +112,9 @@ class SA_ServiceAgent(Agent):
             if late:
                 self.logger.info(f"LATE MSG: SHARED_RESULT from iteration {body['iteration']} client {sender}")
                 return
-            self.recv_committee_shares_pairwise[sender] = json.loads(body["shared_result_pairwise"])
-            self.recv_committee_shares_mi[sender] = json.loads(body["shared_result_mi"])
+            # pairwise shares stay JSON until reconstruction parses them straight into GPU wire rows
+            self.recv_committee_shares_pairwise[sender] = body["shared_result_pairwise"]
+            self.recv_committee_shares_mi[sender] = wire.deserialize_dim1_list(body["shared_result_mi"])
             self.recv_recon_index[sender] = body["committee_member_idx"]
 
     # ---------------------------------------------------------------- round
@@ -119,10 +122,10 @@ class SA_ServiceAgent(Agent):
         t0 = pd.Timestamp("now")
         self.user_committee = param.committee(self.num_clients)
         self.committee_threshold = int(param.fraction * len(self.user_committee))
-        # decryption-key shares for the committee (real Shamir over n; the key itself is a stand-in)
-        system_sk = int.from_bytes(hashlib.sha256(b"flm-system-sk" + param.root_seed).digest(), "big") % self.prime
-        shares = shamir_share(system_sk, max(1, self.committee_threshold), len(self.user_committee), self.prime,
-                              rng=None)
+        # Shamir shares of the system decryption key for the committee (:261-279)
+        pki = param.pki(self.num_clients)
+        shares = shamir_share(pki.system_sk, max(1, self.committee_threshold), len(self.user_committee),
+                              self.prime, rng=None)
         for cnt, cid in enumerate(sorted(self.user_committee)):
             self.sendMessage(cid, Message({"msg": "COMMITTEE_SHARED_SK", "sender": self.id,
                                            "committee_member_idx": cnt + 1, "sk_share": shares[cnt]}),
@@ -171,15 +174,17 @@ class SA_ServiceAgent(Agent):
                 raise RuntimeError("Message lost:", pr)
             self.dec_target_pairwise[pr] = self.pairwise_cipher[pr]
             self.recon_symbol[pr] = sg
-        labels = json.dumps(sorted(offline))
-        self.labels_and_sig = (labels, hashlib.sha256(labels.encode()).hexdigest())  # DSS stand-in
+        # the server signs the offline set (:382-386)
+        labels = json.dumps(sorted(offline)).encode()
+        pki = param.pki(self.num_clients)
+        self.labels_and_sig = (labels, C.ecdsa_sign(pki.server_sk, pki.server_pk, labels))
 
     def report_send_message(self):
         for cnt, cid in enumerate(sorted(self.user_committee)):
             self.sendMessage(cid, Message({
                 "msg": "SIGN", "sender": self.id, "iteration": self.current_iteration,
-                "dec_target_pairwise": json.dumps({json.dumps(list(k)): v for k, v in self.dec_target_pairwise.items()}),
-                "dec_target_mi": json.dumps([self.mi_cipher[c][cnt] for c in self.client_id_list]),
+                "dec_target_pairwise": wire.serialize_dim1_elgamal(self.dec_target_pairwise),
+                "dec_target_mi": wire.serialize_tuples_bytes([self.mi_cipher[c][cnt] for c in self.client_id_list]),
                 "client_id_list": self.client_id_list, "labels": self.labels_and_sig}), tag="comm_dec_server")
 
     def forward_signatures(self, currentTime):
@@ -240,10 +245,18 @@ class SA_ServiceAgent(Agent):
         if not self.dec_target_pairwise:
             self.agent_print("no client dropped out.")
         else:
-            # dropout-pair seeds as returned by the decryptors, in recon_symbol order (:587-603)
-            dec = self.committee_shares_pairwise[members[0]]
-            for pr, sg in self.recon_symbol.items():
-                seeds.append(bytes.fromhex(dec[json.dumps(list(pr))]))
+            # threshold ElGamal decryption of every dropout pair's H, then s = SHA-256(H) (:542-585):
+            # one GPU batch over D pairs x T decryptors
+            c1 = [ct[1] for ct in self.dec_target_pairwise.values()]
+            shares = np.stack([wire.ecp_json_to_wire(self.committee_shares_pairwise[m]) for m in members])
+            if shares.shape[1] != len(c1):
+                raise RuntimeError("length error.")
+            _, pair_seeds, flags = param.engine().ec_combine_wire(C.points_to_wire(c1), shares,
+                                                                  C.scalars_to_wire(coeff))
+            if len(pair_seeds) != len(self.recon_symbol):
+                raise RuntimeError("The decrypted length is wrong.")
+            for s, sg in zip(pair_seeds, self.recon_symbol.values()):
+                seeds.append(bytes(s[: self.key_length]))
                 signs.append(sg)
         # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU
         out = self.vec_sum_partial.astype(np.uint32, copy=True)

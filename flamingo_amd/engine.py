@@ -249,22 +249,56 @@ class MaskEngine:
         return out
 
     # ------------------------------------------------------------ P-256
+    def ec_mul_wire(self, points_w: np.ndarray, scalars_w: np.ndarray):
+        """Batched k_i * P_i on wire arrays: points (n, 64) and scalars (n, 32) uint8 big endian.
+        Returns (out (n, 64) uint8, flags (n,) uint32; bit 2 = infinity, returned as zeros)."""
+        pw = np.ascontiguousarray(points_w, np.uint8).reshape(-1, 64)
+        sw = np.ascontiguousarray(scalars_w, np.uint8).reshape(-1, 32)
+        n = pw.shape[0]
+        if sw.shape[0] != n:
+            raise RuntimeError(f"{sw.shape[0]} scalars for {n} points")
+        out = np.zeros((n, 64), np.uint8)
+        fl = np.zeros(n, np.uint32)
+        if n:
+            self._check(self.lib.flm_ec_mul(self.ctx, p_u8(pw), p_u8(sw), n, p_u8(out), p_u32(fl)), "flm_ec_mul")
+        return out, fl
+
     def ec_mul(self, points, scalars) -> list:
         """[k_i * P_i] for affine points (x, y) and integer scalars (flm_ec_mul).
 
         The ECDH / ElGamal / decryption-share products of SA_ClientAgent.py:256-263,
         :434-447 and :397-400, batched.  Infinity comes back as None."""
         from .crypto import points_from_wire, points_to_wire, scalars_to_wire
-        n = len(points)
-        if len(scalars) != n:
-            raise RuntimeError(f"{len(scalars)} scalars for {n} points")
-        if n == 0:
+        if len(scalars) != len(points):
+            raise RuntimeError(f"{len(scalars)} scalars for {len(points)} points")
+        if not points:
             return []
-        pw, sw = points_to_wire(points), scalars_to_wire(scalars)
-        out = np.zeros((n, 64), np.uint8)
-        fl = np.zeros(n, np.uint32)
-        self._check(self.lib.flm_ec_mul(self.ctx, p_u8(pw), p_u8(sw), n, p_u8(out), p_u32(fl)), "flm_ec_mul")
+        out, fl = self.ec_mul_wire(points_to_wire(points), scalars_to_wire(scalars))
         return points_from_wire(out, fl)
+
+    def ec_combine_wire(self, c1_w, shares_w, lambdas_w, negate: bool = True):
+        """flm_ec_combine on wire arrays: c1 (D, 64) or None, shares (T, D, 64), lambdas (T, 32).
+        Returns (points (D, 64), seeds (D, 32), flags (D,))."""
+        sh = np.ascontiguousarray(shares_w, np.uint8)
+        T = sh.shape[0]
+        lw = np.ascontiguousarray(lambdas_w, np.uint8).reshape(-1, 32)
+        if lw.shape[0] != T:
+            raise RuntimeError(f"{lw.shape[0]} coefficients for {T} share sets")
+        D = c1_w.shape[0] if c1_w is not None else (sh.shape[1] if T else 0)
+        if T and (sh.ndim != 3 or sh.shape[1] != D or sh.shape[2] != 64):
+            raise RuntimeError("shares must be (T, D, 64)")
+        pts = np.zeros((D, 64), np.uint8)
+        seeds = np.zeros((D, 32), np.uint8)
+        fl = np.zeros(D, np.uint32)
+        if D == 0:
+            return pts, seeds, fl
+        cw = np.ascontiguousarray(c1_w, np.uint8) if c1_w is not None else None
+        if not T:
+            sh, lw = np.zeros((1, 64), np.uint8), np.zeros((1, 32), np.uint8)
+        rc = self.lib.flm_ec_combine(self.ctx, p_u8(cw) if cw is not None else None, p_u8(sh), p_u8(lw), T, D,
+                                     1 if negate else 0, p_u8(pts), p_u8(seeds), p_u32(fl))
+        self._check(rc, "flm_ec_combine")
+        return pts, seeds, fl
 
     def ec_combine(self, c1, shares_by_term, lambdas, negate: bool = True):
         """Threshold-ElGamal combine + seed derivation (SA_ServiceAgent.py:542-585).
@@ -280,15 +314,9 @@ class MaskEngine:
             raise RuntimeError("shares must be T lists of D points")
         if D == 0:
             return [], []
-        sh = np.concatenate([points_to_wire(s) for s in shares_by_term]) if T else np.zeros((1, 64), np.uint8)
-        lw = scalars_to_wire(lambdas) if T else np.zeros((1, 32), np.uint8)
-        cw = points_to_wire(c1) if c1 is not None else None
-        pts = np.zeros((D, 64), np.uint8)
-        seeds = np.zeros((D, 32), np.uint8)
-        fl = np.zeros(D, np.uint32)
-        rc = self.lib.flm_ec_combine(self.ctx, p_u8(cw) if cw is not None else None, p_u8(sh), p_u8(lw), T, D,
-                                     1 if negate else 0, p_u8(pts), p_u8(seeds), p_u32(fl))
-        self._check(rc, "flm_ec_combine")
+        sh = np.stack([points_to_wire(s) for s in shares_by_term]) if T else np.zeros((0, D, 64), np.uint8)
+        lw = scalars_to_wire(lambdas) if T else np.zeros((0, 32), np.uint8)
+        pts, seeds, fl = self.ec_combine_wire(points_to_wire(c1) if c1 is not None else None, sh, lw, negate)
         return points_from_wire(pts, fl), [bytes(r) for r in seeds]
 
     def ec_combine_dev(self, c1, shares, lambdas, seeds_out, flags, points_out=None, negate: bool = True,

@@ -1,0 +1,92 @@
+"""The full Flamingo protocol through the ABIDES agents on CPU.
+
+The agents' engine (normally the GPU MaskEngine) is replaced by a test double
+whose methods are the CPU oracle (oracle/oracle.py for masks and sums) and
+the pure-Python / OpenSSL P-256 code (oracle/ec_oracle.py, flamingo_amd.crypto)
+for the scalar multiplications and the threshold combine.  This checks the
+protocol logic -- ECDH keys, h_ijt -> hash-to-curve seeds, ElGamal to the
+system key, committee decryption shares, Lagrange combine, AES-GCM m_i
+shares, JSON payloads -- end to end: the final sum must equal |U| in every
+slot (all-ones inputs, SA_ClientAgent.py:304 + SA_ServiceAgent.py:605),
+with and without dropouts.  The GPU versions of the same runs are in
+tests/test_abides_gpu.py.
+"""
+import numpy as np
+import pytest
+
+import ec_oracle as E
+import oracle as O
+from flamingo_amd import crypto as C
+
+
+class OracleEngine:
+    def client_mask(self, seg, seeds, signs, L, x=None):
+        return O.client_mask(np.asarray(seg, np.int64), np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32),
+                             np.asarray(signs, np.int8), L, x=x)
+
+    def aggregate_unmask(self, vectors, seeds, signs, L=None):
+        rows = np.stack(vectors) if len(vectors) else np.zeros((0, L), np.uint32)
+        sd = np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32) if seeds else np.zeros((0, 32), np.uint8)
+        return O.aggregate_unmask(rows, sd, np.asarray(signs, np.int8), L=L)
+
+    def mask_accumulate(self, seeds, signs, acc, slot0=0):
+        sd = np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32)
+        return acc + O.aggregate_unmask(np.zeros((0, acc.shape[0]), np.uint32), sd, np.asarray(signs, np.int8),
+                                        L=acc.shape[0])
+
+    def chacha20_encrypt(self, key, data, nonce=bytes(8), counter=0):
+        return O.chacha20_encrypt(key, data)
+
+    def ec_mul_wire(self, points_w, scalars_w):
+        pts = C.points_from_wire(points_w)
+        ks = [int.from_bytes(bytes(s), "big") for s in scalars_w]
+        out = [C.mul(k, p) for k, p in zip(ks, pts)]
+        return C.points_to_wire(out), np.array([4 if p is None else 0 for p in out], np.uint32)
+
+    def ec_combine_wire(self, c1_w, shares_w, lambdas_w, negate=True):
+        c1 = C.points_from_wire(c1_w)
+        shares = [C.points_from_wire(s) for s in shares_w]
+        lam = [int.from_bytes(bytes(s), "big") for s in lambdas_w]
+        pts, seeds = E.combine(c1, shares, lam, negate)
+        return (C.points_to_wire(pts), np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32),
+                np.zeros(len(pts), np.uint32))
+
+
+@pytest.fixture
+def oracle_engine(monkeypatch):
+    from flamingo_amd.abides.flamingo import protocol
+    monkeypatch.setattr(protocol, "_engine", OracleEngine())
+    yield
+    protocol.configure(committee=60)
+
+
+@pytest.mark.parametrize("offline", ["", "3,9,20"])
+def test_protocol_end_to_end_on_oracle(oracle_engine, offline):
+    from flamingo_amd.abides.config_flamingo import run
+    argv = ["-c", "flamingo", "-n", "32", "-i", "2", "-s", "5", "-k", "--vector_len", "1000",
+            "--committee_size", "9", "--root_seed_hex", "11" * 32, "--round_time", "30"]
+    if offline:
+        argv += ["--offline", offline]
+    res = run(argv)
+    srv = res["server"]
+    assert sorted(srv.results) == [1, 2]
+    for it, out in srv.results.items():
+        assert np.all(out == srv.online_counts[it]), it
+    if offline:
+        assert len(srv.recon_symbol) > 0 and max(srv.online_counts.values()) <= 29
+
+
+def test_wire_formats_roundtrip():
+    from flamingo_amd.abides.flamingo import wire
+    g2 = C.mul(2)
+    el = {(1, 5): (E.G, g2), (7, 2): (g2, E.G)}
+    s = wire.serialize_dim1_elgamal(el)
+    assert wire.deserialize_dim1_elgamal(s) == el
+    keys, c0, c1 = wire.elgamal_json_to_wire(s)
+    assert keys == [(1, 5), (7, 2)] and C.points_from_wire(c0) == [E.G, g2] and C.points_from_wire(c1) == [g2, E.G]
+    s = wire.serialize_dim1_ecp([E.G, g2])
+    assert wire.deserialize_dim1_ecp(s) == [E.G, g2]
+    assert wire.wire_to_ecp_json(wire.ecp_json_to_wire(s)) == s
+    assert wire.deserialize_dim2_ecp(wire.serialize_dim2_ecp({"a": [E.G]})) == {"a": [E.G]}
+    tb = [(b"\x01\x02", b"\xff" * 16)]
+    assert wire.deserialize_tuples_bytes(wire.serialize_tuples_bytes(tb)) == tb
