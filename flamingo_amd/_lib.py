@@ -46,6 +46,8 @@ SIGNATURES = {
     "flm_ec_combine": (_int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, _u32p]),
     "flm_ec_combine_dev": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _vp, _vp, _vp, _vp]),
     "flm_ec_mul": (_int, [_vp, _u8p, _u8p, _int, _u8p, _u32p]),
+    "flm_shamir_combine": (_int, [_vp, _u8p, _u8p, _int, _int, _u8p]),
+    "flm_shamir_combine_dev": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }

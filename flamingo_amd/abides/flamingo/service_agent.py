@@ -11,9 +11,9 @@ The hot loops are replaced by calls into the MI355X engine:
   reconstruction_process
       s_ij for dropout pairs: c1 - sum_j lambda_j (sk_j c0), SHA-256   (:542-585) -> MaskEngine.ec_combine_wire
       out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> MaskEngine.mask_accumulate
-The vector arithmetic is bit-exact with the reference's numpy uint32 code; m_i
-recovery (Lagrange at 0 over n, :506-526) stays on the host (T x |U| 256-bit
-products).  Message payloads use the reference's JSON formats (wire.py).
+      m_i for online clients: sum_j lambda_j y_{j,i} mod n      (:506-526) -> MaskEngine.shamir_combine
+The vector arithmetic is bit-exact with the reference's numpy uint32 code.
+Message payloads use the reference's JSON formats (wire.py).
 """
 from __future__ import annotations
 
@@ -237,11 +237,9 @@ class SA_ServiceAgent(Agent):
         members = list(self.committee_shares_mi.keys())[: max(1, self.committee_threshold)]
         xs = [self.recon_index[m] for m in members]
         coeff = lagrange_at_zero(xs, self.prime)
-        seeds, signs = [], []
-        for pos, _cid in enumerate(self.client_id_list):
-            mi = sum(c * self.committee_shares_mi[m][pos] for c, m in zip(coeff, members)) % self.prime
-            seeds.append(mi.to_bytes(self.key_length, "big"))
-            signs.append(-1)
+        # m_i = sum_j lambda_j y_{j,i} mod n for every online client, one GPU batch (T x |U|)
+        seeds = param.engine().shamir_combine([self.committee_shares_mi[m] for m in members], coeff)
+        signs = [-1] * len(seeds)
         if not self.dec_target_pairwise:
             self.agent_print("no client dropped out.")
         else:

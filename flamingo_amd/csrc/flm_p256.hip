@@ -123,34 +123,54 @@ __device__ __forceinline__ Fe fe_sub(const Fe &a, const Fe &b) {
     return r;
 }
 
-// Montgomery product a*b*R^-1 mod p (CIOS, quotient digit = low limb since -p^-1 = 1 mod 2^32)
+// acc += a*b with the carry out of the 64-bit accumulator counted in hi: v_mad_u64_u32's own
+// carry-out feeds one v_addc (2 instructions per partial product; measured 673 vs 860 ns per
+// single-wave multiply against a plain 64-bit C formulation, tools/ec_probe.hip)
+__device__ __forceinline__ void mad_acc(uint64_t &acc, uint32_t &hi, uint32_t a, uint32_t b) {
+    uint64_t n, c, d;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(n), "=s"(c) : "v"(a), "v"(b), "v"(acc));
+    asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(hi), "=s"(d) : "v"(hi), "s"(c));
+    acc = n;
+}
+
+// Montgomery product a*b*R^-1 mod p: product scanning (96-bit column accumulator), then the
+// reduction by p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in one signed column pass: the quotient digit
+// m_i is the running limb i itself (-p^-1 = 1 mod 2^32) and adding m_i*p touches limbs
+// i (-m, clears it), i+3 (+m), i+6 (+m), i+7 (-m), i+8 (+m).
 __device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
-    uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t t8 = 0;
+    uint32_t t[16];
+    uint64_t acc = 0;
+    uint32_t hi = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t c = 0;
+    for (int k = 0; k < 15; ++k) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            c = (uint64_t)a.v[j] * b.v[i] + t[j] + (c >> 32);
-            t[j] = (uint32_t)c;
+        for (int i = 0; i < 8; ++i) {
+            int j = k - i;
+            if (j < 0 || j > 7) continue;
+            mad_acc(acc, hi, a.v[i], b.v[j]);
         }
-        uint64_t s = (uint64_t)t8 + (c >> 32);
-        uint32_t hi0 = (uint32_t)s, hi1 = (uint32_t)(s >> 32);
-        uint32_t m = t[0];
-        // (t + m*p) / 2^32 with p's limbs {-1,-1,-1,0,0,0,1,-1}
-        c = (uint64_t)m * kP[0] + t[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            c = (uint64_t)m * kP[j] + t[j] + (c >> 32);
-            t[j - 1] = (uint32_t)c;
-        }
-        s = (uint64_t)hi0 + (c >> 32);
-        t[7] = (uint32_t)s;
-        t8 = hi1 + (uint32_t)(s >> 32);
+        t[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)hi << 32);
+        hi = 0;
     }
+    t[15] = (uint32_t)acc;
+    uint32_t m[8];
+    int64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int64_t s = (int64_t)t[i] + carry;
+        if (i >= 3 && i - 3 < 8) s += m[i - 3];
+        if (i >= 6 && i - 6 < 8) s += m[i - 6];
+        if (i >= 7 && i - 7 < 8) s -= m[i - 7];
+        if (i >= 8 && i - 8 < 8) s += m[i - 8];
+        if (i < 8) m[i] = (uint32_t)s; else t[i - 8] = (uint32_t)s;
+        carry = s >> 32;
+    }
+    uint32_t r8[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r8[i] = t[i];
     Fe r;
-    fe_reduce_once(r, t, t8);
+    fe_reduce_once(r, r8, (uint32_t)carry);
     return r;
 }
 
@@ -400,18 +420,21 @@ __device__ __forceinline__ Jac load_jac(const uint32_t *jac, size_t plane_stride
     return R;
 }
 
-// Scalar multiplication scalar * point for T x D (term, element) pairs.
-// points: [T][D][64] wire bytes; scalars: [T][32] (one per term, uniform over a
-// workgroup) or [T][D][32] when per_element; jac out: SoA planes [T][24][D].
+// Scalar multiplication scalar * point for T x D (term, element) pairs, flattened to one lane
+// per pair g = j*D + i (1-D grid; the workgroup size is a launch parameter).
+// points: [T][D][64] wire bytes; scalars: [T][32] (one per term) or [T][D][32] when
+// per_element; jac out: SoA planes [T][24][D].
 // Fixed 4-bit windows from the most significant nibble; 4 doublings + 1 add per window.
-__global__ __launch_bounds__(kEcThreads) void ec_mul_kernel(const uint8_t *__restrict__ points,
-                                                            const uint8_t *__restrict__ scalars, int per_element,
-                                                            int D, uint32_t *__restrict__ jac,
-                                                            uint32_t *__restrict__ flags) {
-    const int j = blockIdx.y;
-    const int i = blockIdx.x * kEcThreads + threadIdx.x;
-    if (i >= D) return;
-    const size_t e = (size_t)j * D + i;
+template <int TPB>
+__global__ __launch_bounds__(TPB) void ec_mul_kernel(const uint8_t *__restrict__ points,
+                                                     const uint8_t *__restrict__ scalars, int per_element, int T,
+                                                     int D, uint32_t *__restrict__ jac,
+                                                     uint32_t *__restrict__ flags) {
+    const size_t g = (size_t)blockIdx.x * TPB + threadIdx.x;
+    if (g >= (size_t)T * D) return;
+    const int j = (int)(g / D);
+    const int i = (int)(g - (size_t)j * D);
+    const size_t e = g;
     Jac P;
     bool ok = load_point(points + e * 64, P);
     if (!ok) atomicOr(&flags[i], 2u);
@@ -482,14 +505,120 @@ __global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__
     if (fl) atomicOr(&flags[i], fl);
 }
 
+// ------------------------------------------------- scalar field (mod n)
+// Shamir recovery of the self-mask seeds (SA_ServiceAgent.py:506-526):
+//     m_i = sum_j lambda_j * y_{j,i} mod n,   seed_i = m_i.to_bytes(32, 'big')
+// with n the P-256 group order (the reference's `prime`, ecchash.n).  Generic
+// CIOS Montgomery (n has no special form); T multiplications per lane.
+__device__ constexpr uint32_t kN[8] = {0xfc632551u, 0xf3b9cac2u, 0xa7179e84u, 0xbce6faadu,
+                                       0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu};
+__device__ constexpr uint32_t kR2N[8] = {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 0x4699799cu,
+                                         0x2b6bec59u, 0x2845b239u, 0xf3d95620u, 0x66e12d94u};  // R^2 mod n
+constexpr uint32_t kN0 = 0xee00bc4fu;                                                             // -n^-1 mod 2^32
+
+__device__ __forceinline__ void sc_reduce_once(Fe &r, const uint32_t (&t)[8], uint32_t t8) {
+    uint32_t d[8];
+    uint64_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t x = (uint64_t)t[i] - kN[i] - b;
+        d[i] = (uint32_t)x;
+        b = x >> 63;
+    }
+    bool take = t8 || !b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = take ? d[i] : t[i];
+}
+
+__device__ __forceinline__ Fe sc_mul(const Fe &a, const Fe &b) {
+    uint32_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t t8 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c = (uint64_t)a.v[j] * b.v[i] + t[j] + (c >> 32);
+            t[j] = (uint32_t)c;
+        }
+        uint64_t s = (uint64_t)t8 + (c >> 32);
+        uint32_t hi0 = (uint32_t)s, hi1 = (uint32_t)(s >> 32);
+        uint32_t m = t[0] * kN0;
+        c = (uint64_t)m * kN[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            c = (uint64_t)m * kN[j] + t[j] + (c >> 32);
+            t[j - 1] = (uint32_t)c;
+        }
+        s = (uint64_t)hi0 + (c >> 32);
+        t[7] = (uint32_t)s;
+        t8 = hi1 + (uint32_t)(s >> 32);
+    }
+    Fe r;
+    sc_reduce_once(r, t, t8);
+    return r;
+}
+
+__device__ __forceinline__ Fe sc_add(const Fe &a, const Fe &b) {
+    uint32_t s[8];
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c = (uint64_t)a.v[i] + b.v[i] + (c >> 32);
+        s[i] = (uint32_t)c;
+    }
+    Fe r;
+    sc_reduce_once(r, s, (uint32_t)(c >> 32));
+    return r;
+}
+
+// shares: [T][M][32] big endian; lambdas: [T][32]; out: [M][32] big endian
+__global__ __launch_bounds__(kEcThreads) void shamir_combine_kernel(const uint8_t *__restrict__ shares,
+                                                                    const uint8_t *__restrict__ lambdas, int T,
+                                                                    int M, uint8_t *__restrict__ out) {
+    const int i = blockIdx.x * kEcThreads + threadIdx.x;
+    if (i >= M) return;
+    Fe acc = {};
+    const Fe r2 = fe_const(kR2N);
+#pragma unroll 1
+    for (int j = 0; j < T; ++j) {
+        Fe y = load_be(shares + ((size_t)j * M + i) * 32);
+        Fe z = {};
+        y = sc_add(y, z);                                   // y < 2^256 < 2n: one subtraction makes y < n
+        Fe lm = sc_mul(load_be(lambdas + (size_t)j * 32), r2);   // lambda * R mod n
+        acc = sc_add(acc, sc_mul(lm, y));                   // lambda * y mod n
+    }
+    store_be(out + (size_t)i * 32, acc);
+}
+
 }  // namespace
 
 hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
-                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream) {
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads) {
     if (T <= 0 || D <= 0) return hipSuccess;
-    dim3 grid((D + kEcThreads - 1) / kEcThreads, T);
-    hipLaunchKernelGGL(ec_mul_kernel, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, per_element, D, d_jac,
-                       d_flags);
+    const size_t n = (size_t)T * D;
+    switch (threads) {
+        case 64:
+            hipLaunchKernelGGL(ec_mul_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, stream, d_points,
+                               d_scalars, per_element, T, D, d_jac, d_flags);
+            break;
+        case 128:
+            hipLaunchKernelGGL(ec_mul_kernel<128>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, stream, d_points,
+                               d_scalars, per_element, T, D, d_jac, d_flags);
+            break;
+        default:
+            hipLaunchKernelGGL(ec_mul_kernel<256>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, d_points,
+                               d_scalars, per_element, T, D, d_jac, d_flags);
+            break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_shamir_combine(const uint8_t *d_shares, const uint8_t *d_lambdas, int T, int M, uint8_t *d_out,
+                                 hipStream_t stream) {
+    if (M <= 0) return hipSuccess;
+    dim3 grid((M + kEcThreads - 1) / kEcThreads);
+    hipLaunchKernelGGL(shamir_combine_kernel, grid, dim3(kEcThreads), 0, stream, d_shares, d_lambdas, T, M, d_out);
     return hipGetLastError();
 }
 

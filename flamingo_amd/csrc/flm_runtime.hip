@@ -92,6 +92,7 @@ struct flm_ctx {
     int table_k = -1;  // seeds in the current device seed table
     int tune_variant = -1;   // items_kernel variant, -1 = auto
     int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
+    int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
 };
 
@@ -799,6 +800,10 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
         if (value != 0 && value != 1 && value != 4 && value != 16)
             return fail(ctx, FLM_EINVAL, "subtiles must be 0 (auto), 1, 4 or 16");
         ctx->tune_subtiles = value;
+    } else if (k == "ec_threads") {
+        if (value != 64 && value != 128 && value != 256)
+            return fail(ctx, FLM_EINVAL, "ec_threads must be 64, 128 or 256");
+        ctx->tune_ec_threads = value;
     } else {
         return fail(ctx, FLM_EINVAL, "unknown tuning key '%s'", key);
     }
@@ -844,7 +849,8 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
-    FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s));
+    FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
+                                    ctx->tune_ec_threads));
     FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), T, D, negate, d_points_out, d_seeds_out,
                                        d_flags, s));
     return 0;
@@ -887,6 +893,40 @@ int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const
     return 0;
 }
 
+int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t *d_lambdas, int T, int M,
+                           uint8_t *d_seeds_out, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, T, M)) return rc;
+    if (M == 0) return 0;
+    if (!d_seeds_out || (T > 0 && (!d_shares || !d_lambdas))) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    FLM_HIP(ctx, flm::launch_shamir_combine(d_shares, d_lambdas, T, M, d_seeds_out, s));
+    return 0;
+}
+
+int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambdas, int T, int M,
+                       uint8_t *seeds_out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, T, M)) return rc;
+    if (M == 0) return 0;
+    if (!seeds_out || (T > 0 && (!shares || !lambdas))) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    FLM_HIP(ctx, ctx->ec_in.reserve((size_t)std::max(T, 1) * M * 32));
+    FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)std::max(T, 1) * 32));
+    FLM_HIP(ctx, ctx->ec_dig.reserve((size_t)M * 32));
+    if (T > 0) {
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, shares, (size_t)T * M * 32, hipMemcpyHostToDevice, s));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lambdas, (size_t)T * 32, hipMemcpyHostToDevice, s));
+    }
+    FLM_HIP(ctx, flm::launch_shamir_combine(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), T, M,
+                                            ctx->ec_dig.as<uint8_t>(), s));
+    FLM_HIP(ctx, hipMemcpyAsync(seeds_out, ctx->ec_dig.p, (size_t)M * 32, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipStreamSynchronize(s));
+    return 0;
+}
+
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out) {
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (int rc = ec_dims(ctx, 1, n)) return rc;
@@ -903,7 +943,8 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, scalars, (size_t)n * 32, hipMemcpyHostToDevice, s));
     FLM_HIP(ctx, hipMemsetAsync(ctx->ec_flags.p, 0, (size_t)n * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), 1, 1, n,
-                                    ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s));
+                                    ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s,
+                                    ctx->tune_ec_threads));
     FLM_HIP(ctx, flm::launch_ec_finish(nullptr, ctx->ec_jac.as<uint32_t>(), 1, n, 0, ctx->ec_out.as<uint8_t>(),
                                        nullptr, ctx->ec_flags.as<uint32_t>(), s));
     std::vector<uint32_t> fl(n);

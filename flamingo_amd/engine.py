@@ -319,6 +319,33 @@ class MaskEngine:
         pts, seeds, fl = self.ec_combine_wire(points_to_wire(c1) if c1 is not None else None, sh, lw, negate)
         return points_from_wire(pts, fl), [bytes(r) for r in seeds]
 
+    def shamir_combine(self, shares_by_term, lambdas) -> list:
+        """m_i = sum_j lambda_j y_{j,i} mod n as 32-byte big-endian seeds (SA_ServiceAgent.py:506-526).
+        shares_by_term: T sequences of M integers (< 2^256); lambdas: T integers (< n)."""
+        from .crypto import scalars_to_wire
+        T = len(lambdas)
+        if len(shares_by_term) != T:
+            raise RuntimeError(f"{len(shares_by_term)} share lists for {T} coefficients")
+        M = len(shares_by_term[0]) if T else 0
+        if any(len(s) != M for s in shares_by_term):
+            raise RuntimeError("share lists differ in length")
+        if M == 0:
+            return []
+        sh = np.stack([scalars_to_wire(s) for s in shares_by_term])
+        out = np.zeros((M, 32), np.uint8)
+        rc = self.lib.flm_shamir_combine(self.ctx, p_u8(sh), p_u8(scalars_to_wire(lambdas)), T, M, p_u8(out))
+        self._check(rc, "flm_shamir_combine")
+        return [bytes(r) for r in out]
+
+    def shamir_combine_dev(self, shares, lambdas, seeds_out, stream=None):
+        """Device form: shares (T, M, 32), lambdas (T, 32) uint8 CUDA tensors -> seeds_out (M, 32)."""
+        T, M = shares.shape[0], shares.shape[1]
+        rc = self.lib.flm_shamir_combine_dev(self.ctx, ctypes.c_void_p(shares.data_ptr()),
+                                             ctypes.c_void_p(lambdas.data_ptr()), T, M,
+                                             ctypes.c_void_p(seeds_out.data_ptr()), self._stream_handle(stream))
+        self._check(rc, "flm_shamir_combine_dev")
+        return seeds_out
+
     def ec_combine_dev(self, c1, shares, lambdas, seeds_out, flags, points_out=None, negate: bool = True,
                        stream=None):
         """Device form: c1 (D,64), shares (T,D,64), lambdas (T,32) uint8 CUDA tensors;

@@ -145,7 +145,9 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "subtiles" 0 auto | 1 | 4 | 16 sub-tiles of 1024 slots per workgroup
  *              for aggregate plans.
  *   "pairing"  0 interleaved single-kind items | 1 dual-tile items (default), for
- *              windows where rows and masks cover different tiles. */
+ *              windows where rows and masks cover different tiles.
+ *   "ec_threads" 64 (default) | 128 | 256 lanes per workgroup of the P-256
+ *              scalar-multiplication kernel. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the
@@ -184,6 +186,17 @@ int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const
 int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_shares, const uint8_t *d_lambdas, int T,
                        int D, int negate, uint8_t *d_points_out, uint8_t *d_seeds_out, uint32_t *d_flags,
                        void *stream);
+/* Shamir recovery of the self-mask seeds (SA_ServiceAgent.py:506-526):
+ *   seed_i = (sum_{j<T} lambdas[j] * shares[j][i] mod n).to_bytes(32, 'big')
+ * for i < M (M = |U| online clients), n = the P-256 group order (ecchash.n),
+ * shares[j][i] = committee member j's decrypted share of m_i as a 32-byte
+ * big-endian integer (any value < 2^256), lambdas[j] < n the Lagrange
+ * coefficients at 0.  shares: T*M*32 bytes, term-major.  The seeds are the
+ * ChaCha20 keys of the self masks (sign -1), ready for flm_seed_table_dev. */
+int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambdas, int T, int M,
+                       uint8_t *seeds_out);
+int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t *d_lambdas, int T, int M,
+                           uint8_t *d_seeds_out, void *stream);
 /* Batched scalar multiplication out[i] = scalars[i] * points[i]: the ECDH
  * (SA_ClientAgent.py:256-263), ElGamal (:434-447) and decryption-share
  * (:397-400) products, n independent elements per call. */

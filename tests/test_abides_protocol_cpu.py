@@ -43,6 +43,11 @@ class OracleEngine:
         out = [C.mul(k, p) for k, p in zip(ks, pts)]
         return C.points_to_wire(out), np.array([4 if p is None else 0 for p in out], np.uint32)
 
+    def shamir_combine(self, shares_by_term, lambdas):
+        M = len(shares_by_term[0]) if lambdas else 0
+        return [(sum(l * s[i] for l, s in zip(lambdas, shares_by_term)) % E.N).to_bytes(32, "big")
+                for i in range(M)]
+
     def ec_combine_wire(self, c1_w, shares_w, lambdas_w, negate=True):
         c1 = C.points_from_wire(c1_w)
         shares = [C.points_from_wire(s) for s in shares_w]

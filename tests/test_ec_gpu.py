@@ -124,3 +124,23 @@ def test_ec_combine_dev_feeds_seed_table(eng):
                                np.uint8).reshape(33, 32)
     assert np.array_equal(seeds_t.cpu().numpy(), want_seeds)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), O.aggregate_unmask(rows, want_seeds, signs))
+
+
+def test_shamir_combine_matches_bigint(eng):
+    """m_i = sum_j lambda_j y_{j,i} mod n (SA_ServiceAgent.py:506-526) against Python big ints."""
+    from flamingo_amd.abides.flamingo.seeds import lagrange_at_zero, shamir_share
+    rng = random.Random(17)
+    T, M = 20, 300
+    secrets_ = [rng.randrange(0, 2**256) for _ in range(M)]
+    pts = [shamir_share(s, T, 60, rng=rng) for s in secrets_]
+    chosen = sorted(rng.sample(range(60), T))
+    lam = lagrange_at_zero([c + 1 for c in chosen])
+    shares = [[pts[i][c][1] for i in range(M)] for c in chosen]
+    got = eng.shamir_combine(shares, lam)
+    assert got == [(s % E.N).to_bytes(32, "big") for s in secrets_]
+    # edge values: y >= n, y = 2^256 - 1, lambda in {0, 1, n - 1}
+    ys = [[E.N, E.N + 5, 2**256 - 1, 0, 1], [E.N - 1, 2**255, 7, 2**256 - 1, 0], [3, 3, 3, 3, 3]]
+    ls = [0, 1, E.N - 1]
+    want = [(sum(l * y[i] for l, y in zip(ls, ys)) % E.N).to_bytes(32, "big") for i in range(5)]
+    assert eng.shamir_combine(ys, ls) == want
+    assert eng.shamir_combine([], []) == []

@@ -5,8 +5,12 @@ random points (scalar multiples of G) made by OpenSSL; the GPU result is
 checked against OpenSSL's sum for a few pairs."""
 import argparse
 import json
+import os
 import random
+import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import numpy as np
 import torch
@@ -19,15 +23,22 @@ ap.add_argument("--D", type=int, default=1000)
 ap.add_argument("--T", type=int, default=20)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--cpu-sample", type=int, default=100, help="scalar mults timed on the host")
+ap.add_argument("--threads", type=int, default=64)
+ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
 a = ap.parse_args()
 
 rng = random.Random(1)
 base = [C.mul(rng.randrange(1, C.N)) for _ in range(64)]
 shares = np.stack([C.points_to_wire([base[(j * 7 + i) % 64] for i in range(a.D)]) for j in range(a.T)])
-lams = [rng.randrange(1, C.N) for _ in range(a.T)]
+if a.scalars == "lagrange":
+    from flamingo_amd.abides.flamingo.seeds import lagrange_at_zero
+    lams = lagrange_at_zero(sorted(rng.sample(range(1, 61), a.T)))
+else:
+    lams = [rng.randrange(1, C.N) for _ in range(a.T)]
 c1 = C.points_to_wire([base[(i * 3) % 64] for i in range(a.D)])
 dev = torch.device("cuda:0")
 eng = MaskEngine(0)
+eng.set_tuning("ec_threads", a.threads)
 c1_t = torch.from_numpy(c1).to(dev)
 sh_t = torch.from_numpy(shares).to(dev)
 lam_t = torch.from_numpy(C.scalars_to_wire(lams)).to(dev)
@@ -57,7 +68,7 @@ t = time.perf_counter()
 for i in range(a.cpu_sample):
     C.mul(lams[i % a.T], base[i % 64])
 cpu_per_mul = (time.perf_counter() - t) / a.cpu_sample
-print(json.dumps({"D": a.D, "T": a.T, "gpu_ms": round(gpu_ms, 4),
+print(json.dumps({"threads": a.threads, "D": a.D, "T": a.T, "scalars": a.scalars, "lambda_hex": [hex(x)[:12] for x in lams[:4]], "gpu_ms": round(gpu_ms, 4),
                   "gpu_scalar_mults_per_s": round(a.D * a.T / gpu_ms * 1e3),
                   "cpu_openssl_ms_est": round(cpu_per_mul * a.D * a.T * 1e3, 1),
                   "cpu_openssl_us_per_mul": round(cpu_per_mul * 1e6, 1), "cpu_cores": 1}))
