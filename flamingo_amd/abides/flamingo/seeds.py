@@ -1,24 +1,20 @@
-"""Seed transport for the Flamingo agents: real Shamir sharing, stand-in encryption.
+"""Shamir secret sharing over the P-256 group order (util/crypto/secretsharing).
 
-The reference protects the two kinds of mask seeds with public-key crypto:
-* self-mask seed m_i: Shamir-shared over the P-256 group order n to the
-  committee, each share AES-GCM encrypted under an ECDH key
-  (SA_ClientAgent.py:214-244); the server Lagrange-interpolates the first
-  `threshold` decrypted shares (SA_ServiceAgent.py:506-526).
-* pairwise seed s_ij: ECDH -> SHA-256 -> ChaCha20 PRF of the iteration ->
-  hash-to-curve -> SHA-256 (SA_ClientAgent.py:256-292), ElGamal-encrypted to
-  the committee's threshold key and decrypted only for dropout pairs
-  (SA_ServiceAgent.py:542-585).
+The reference shares two secrets this way:
+* each client's self-mask seed m_i, dealt to the committee
+  (SA_ClientAgent.py:214-244) and recovered by the server from the first
+  `threshold` decrypted shares (SA_ServiceAgent.py:506-526; on the GPU:
+  MaskEngine.shamir_combine);
+* the system decryption key, dealt by the server at setup
+  (SA_ServiceAgent.py:259-279), whose Lagrange coefficients also drive the
+  threshold-ElGamal combine (:542-585; on the GPU: MaskEngine.ec_combine_wire).
 
-Those EC/AES steps are outside this repository's hot path.
-Here the Shamir sharing and Lagrange recovery of m_i are real (mod n, so the
-reference's m_i mod n behaviour is kept), while share "encryption" and the
-pairwise-seed derivation are explicit stand-ins: shares travel as integers and
-s_ij = SHA-256(b"flm-pair" || root || iteration || min(i,j) || max(i,j)).
+secret_int_to_points / points_to_secret_int / modular_lagrange_interpolation
+(secretsharing/sharing.py:20-57, polynomials.py:31-109) restated: points at
+x = 1..num_points, all arithmetic mod n.
 """
 from __future__ import annotations
 
-import hashlib
 import secrets
 
 # P-256 group order (the `prime` the reference shares over: ecchash.n)
@@ -56,10 +52,3 @@ def lagrange_at_zero(xs, prime: int = P256_N):
 def shamir_recover(points, prime: int = P256_N) -> int:
     xs = [x for x, _ in points]
     return sum(l * y for l, (_, y) in zip(lagrange_at_zero(xs, prime), points)) % prime
-
-
-def pair_seed(root_seed: bytes, iteration: int, i: int, j: int) -> bytes:
-    """Stand-in for the reference's s_ij (symmetric in i, j; new every iteration)."""
-    a, b = (i, j) if i < j else (j, i)
-    return hashlib.sha256(b"flm-pair" + root_seed + iteration.to_bytes(8, "big") + a.to_bytes(4, "big")
-                          + b.to_bytes(4, "big")).digest()

@@ -5,7 +5,7 @@ import pandas as pd
 import pytest
 
 from flamingo_amd.abides import Agent, Kernel, LatencyModel, Message
-from flamingo_amd.abides.flamingo.seeds import P256_N, lagrange_at_zero, pair_seed, shamir_recover, shamir_share
+from flamingo_amd.abides.flamingo.seeds import P256_N, lagrange_at_zero, shamir_recover, shamir_share
 
 
 class Recorder(Agent):
@@ -99,7 +99,23 @@ def test_shamir_roundtrip_and_threshold():
     assert sum(lagrange_at_zero(xs)) % P256_N == 1            # interpolates constants exactly
 
 
-def test_pair_seed_symmetric_and_fresh():
-    r = bytes(32)
-    assert pair_seed(r, 1, 3, 9) == pair_seed(r, 1, 9, 3)
-    assert pair_seed(r, 1, 3, 9) != pair_seed(r, 2, 3, 9)
+def test_pair_seed_pipeline_symmetric():
+    """s_ij derived by i (a_i A_j) equals the one derived by j (a_j A_i) (SA_ClientAgent.py:256-292).
+
+    Reference quirk kept: h_ijt = ChaCha20(key).encrypt(t.to_bytes(16, 'big'))[0:4] & 0xFFFF
+    (:276-279) only sees keystream bytes 0-3 XOR the zero high bytes of t, so s_ij is the
+    same in every iteration t < 2^96, and differs only between pairs."""
+    import hashlib
+    from flamingo_amd import crypto as C
+    ai, aj = 1234567, 7654321
+    Ai, Aj = C.mul(ai), C.mul(aj)
+
+    def seed(a, B, it):
+        key = hashlib.sha256(C.point_bytes(C.mul(a, B))).digest()
+        h = C.chacha20_encrypt(key, it.to_bytes(16, "big"))
+        H = C.hash_str_to_curve(str(int.from_bytes(h[:4], "big") & 0xFFFF))
+        return hashlib.sha256(C.point_bytes(H)).digest()
+
+    assert seed(ai, Aj, 1) == seed(aj, Ai, 1)
+    assert seed(ai, Aj, 1) == seed(ai, Aj, 2)
+    assert seed(ai, Aj, 1) != seed(ai, C.mul(99), 1)

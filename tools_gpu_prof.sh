@@ -13,3 +13,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_ou
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_${TAG}_pmc2 -o run -- $B > $R/gpurun_out/prof_${TAG}_pmc2.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_INSTS_SALU --output-format csv -d $R/gpurun_out/prof_${TAG}_pmc3 -o run -- $B > $R/gpurun_out/prof_${TAG}_pmc3.log 2>&1 || exit $?
 cd $R && python3 tools/summarize_profile.py gpurun_out/prof_${TAG}_summary.json gpurun_out/prof_${TAG}_trace gpurun_out/prof_${TAG}_pmc1 gpurun_out/prof_${TAG}_pmc2 gpurun_out/prof_${TAG}_pmc3 > /dev/null
+# seed recovery (c5 shape): kernel trace + stats of tools/recovery_bench.py
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_recovery -o run -- python3 $R/tools/recovery_bench.py > $R/gpurun_out/prof_${TAG}_recovery.log 2>&1 || exit $?
