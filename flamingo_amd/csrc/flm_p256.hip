@@ -124,36 +124,22 @@ __device__ __forceinline__ Fe fe_sub(const Fe &a, const Fe &b) {
 }
 
 // acc += a*b with the carry out of the 64-bit accumulator counted in hi: v_mad_u64_u32's own
-// carry-out feeds one v_addc (2 instructions per partial product; measured 673 vs 860 ns per
-// single-wave multiply against a plain 64-bit C formulation, tools/ec_probe.hip)
+// carry-out feeds one v_addc, both in ONE asm statement.  Split across two statements the
+// compiler pads every boundary with s_nop (it cannot see through inline asm); together they
+// issue back to back.  tools/ec_probe.hip: 543 ns per single-wave multiply, against 669 ns
+// with the pads and 860 ns for a plain 64-bit C CIOS; bit-identical on 65536 inputs.
 __device__ __forceinline__ void mad_acc(uint64_t &acc, uint32_t &hi, uint32_t a, uint32_t b) {
-    uint64_t n, c, d;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(n), "=s"(c) : "v"(a), "v"(b), "v"(acc));
-    asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(hi), "=s"(d) : "v"(hi), "s"(c));
-    acc = n;
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+        "v_addc_co_u32_e64 %1, %2, 0, %1, %2"
+        : "+v"(acc), "+v"(hi), "=&s"(c)
+        : "v"(a), "v"(b));
 }
 
-// Montgomery product a*b*R^-1 mod p: product scanning (96-bit column accumulator), then the
-// reduction by p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in one signed column pass: the quotient digit
-// m_i is the running limb i itself (-p^-1 = 1 mod 2^32) and adding m_i*p touches limbs
-// i (-m, clears it), i+3 (+m), i+6 (+m), i+7 (-m), i+8 (+m).
-__device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
-    uint32_t t[16];
-    uint64_t acc = 0;
-    uint32_t hi = 0;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int j = k - i;
-            if (j < 0 || j > 7) continue;
-            mad_acc(acc, hi, a.v[i], b.v[j]);
-        }
-        t[k] = (uint32_t)acc;
-        acc = (acc >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
-    }
-    t[15] = (uint32_t)acc;
+// Montgomery reduction of a 512-bit product t by p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in one
+// signed column pass: the quotient digit m_i is the running limb i itself (-p^-1 = 1 mod
+// 2^32) and adding m_i*p touches limbs i (-m, clears it), i+3 (+m), i+6 (+m), i+7 (-m), i+8 (+m).
+__device__ __forceinline__ Fe mont_reduce(uint32_t (&t)[16]) {
     uint32_t m[8];
     int64_t carry = 0;
 #pragma unroll
@@ -174,7 +160,53 @@ __device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
     return r;
 }
 
-__device__ __forceinline__ Fe fe_sqr(const Fe &a) { return fe_mul(a, a); }
+// Montgomery product a*b*R^-1 mod p: product scanning with a 96-bit column accumulator
+__device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
+    uint32_t t[16];
+    uint64_t acc = 0;
+    uint32_t hi = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int j = k - i;
+            if (j < 0 || j > 7) continue;
+            mad_acc(acc, hi, a.v[i], b.v[j]);
+        }
+        t[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)hi << 32);
+        hi = 0;
+    }
+    t[15] = (uint32_t)acc;
+    return mont_reduce(t);
+}
+
+// a^2 R^-1: 28 cross products summed once and doubled, plus 8 squares (36 mads instead of 64)
+__device__ __forceinline__ Fe fe_sqr(const Fe &a) {
+    uint32_t t[16];
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+        uint64_t x = 0;
+        uint32_t xh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int j = k - i;
+            if (j <= i || j > 7) continue;
+            mad_acc(x, xh, a.v[i], a.v[j]);
+        }
+        xh = (xh << 1) | (uint32_t)(x >> 63);
+        x <<= 1;
+        uint64_t n = x + c;
+        xh += (n < x);
+        x = n;
+        if ((k & 1) == 0) mad_acc(x, xh, a.v[k / 2], a.v[k / 2]);
+        t[k] = (uint32_t)x;
+        c = (x >> 32) | ((uint64_t)xh << 32);
+    }
+    t[15] = (uint32_t)c;
+    return mont_reduce(t);
+}
 
 __device__ __forceinline__ Fe fe_neg(const Fe &a) {
     Fe z = {};

@@ -225,6 +225,68 @@ template <> __device__ __forceinline__ Fe fe_mul<6>(const Fe &a, const Fe &b) {
     return mont_special(t);
 }
 
+// two products into two accumulators in ONE asm block: each carry is read one instruction
+// after it is written, and no compiler s_nop pads between asm statements
+__device__ __forceinline__ void mad_acc2(uint64_t &A, uint32_t &hA, uint64_t &B, uint32_t &hB, uint32_t a0,
+                                         uint32_t b0, uint32_t a1, uint32_t b1) {
+    uint64_t cA, cB;
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %8, %9, %1\n\t"
+        "v_addc_co_u32_e64 %2, %4, 0, %2, %4\n\t"
+        "v_addc_co_u32_e64 %3, %5, 0, %3, %5"
+        : "+v"(A), "+v"(B), "+v"(hA), "+v"(hB), "=&s"(cA), "=&s"(cB)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+
+// single chain, mad and addc back to back in one block (tests whether a wait state is needed)
+__device__ __forceinline__ void mad_acc1(uint64_t &A, uint32_t &hA, uint32_t a0, uint32_t b0) {
+    uint64_t cA;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+        "v_addc_co_u32_e64 %1, %2, 0, %1, %2"
+        : "+v"(A), "+v"(hA), "=&s"(cA)
+        : "v"(a0), "v"(b0));
+}
+
+template <int PAIRED>
+__device__ __forceinline__ void product_cols(const Fe &a, const Fe &b, uint32_t (&t)[16]) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+        uint64_t A = carry, B = 0;
+        uint32_t hA = 0, hB = 0;
+        int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+        int n = hi - lo + 1;
+        if (PAIRED) {
+#pragma unroll
+            for (int q = 0; q + 1 < n; q += 2)
+                mad_acc2(A, hA, B, hB, a.v[lo + q], b.v[k - lo - q], a.v[lo + q + 1], b.v[k - lo - q - 1]);
+            if (n & 1) mad_acc1(A, hA, a.v[hi], b.v[k - hi]);
+            uint64_t s = A + B;
+            uint32_t h = hA + hB + (s < A);
+            t[k] = (uint32_t)s;
+            carry = (s >> 32) | ((uint64_t)h << 32);
+        } else {
+#pragma unroll
+            for (int q = 0; q < n; ++q) mad_acc1(A, hA, a.v[lo + q], b.v[k - lo - q]);
+            t[k] = (uint32_t)A;
+            carry = (A >> 32) | ((uint64_t)hA << 32);
+        }
+    }
+    t[15] = (uint32_t)carry;
+}
+
+template <> __device__ __forceinline__ Fe fe_mul<7>(const Fe &a, const Fe &b) {
+    uint32_t t[16];
+    product_cols<1>(a, b, t);
+    return mont_special(t);
+}
+
+template <> __device__ __forceinline__ Fe fe_mul<8>(const Fe &a, const Fe &b) {
+    uint32_t t[16];
+    product_cols<0>(a, b, t);
+    return mont_special(t);
+}
+
 template <int V>
 __global__ __launch_bounds__(64) void mul_chain(Fe *x, const Fe *y, int reps) {
     int i = blockIdx.x * 64 + threadIdx.x;
@@ -280,11 +342,13 @@ __global__ void check_variants(const Fe *x, const Fe *y, int *bad) {
     // bring inputs below p first
     a = fe_mul<0>(a, a);
     b = fe_mul<0>(b, a);
-    Fe r0 = fe_mul<0>(a, b), r1 = fe_mul<1>(a, b), r3 = fe_mul<3>(a, b), r4 = fe_mul<4>(a, b), r6 = fe_mul<6>(a, b);
+    Fe r0 = fe_mul<0>(a, b), r1 = fe_mul<1>(a, b), r3 = fe_mul<3>(a, b), r4 = fe_mul<4>(a, b), r6 = fe_mul<6>(a, b), r7 = fe_mul<7>(a, b),
+       r8 = fe_mul<8>(a, b);
     Fe s0 = fe_mul<0>(a, a), s5 = fe_mul<5>(a, a);
     int e = 0;
     for (int k = 0; k < 8; ++k) e |= (r0.v[k] != r1.v[k]) | (r0.v[k] != r3.v[k]) << 1 | (r0.v[k] != r4.v[k]) << 2 |
-                                     (s0.v[k] != s5.v[k]) << 3 | (r0.v[k] != r6.v[k]) << 4;
+                                     (s0.v[k] != s5.v[k]) << 3 | (r0.v[k] != r6.v[k]) << 4 |
+                                     (r0.v[k] != r7.v[k]) << 5 | (r0.v[k] != r8.v[k]) << 6;
     if (e) atomicOr(bad, e);
 }
 
@@ -333,11 +397,14 @@ int main() {
         float t4 = timeit([&] { hipLaunchKernelGGL(mul_chain<4>, dim3(blk), dim3(64), 0, 0, x, y, reps); });
         float t5 = timeit([&] { hipLaunchKernelGGL(mul_chain<5>, dim3(blk), dim3(64), 0, 0, x, y, reps); });
         float t6 = timeit([&] { hipLaunchKernelGGL(mul_chain<6>, dim3(blk), dim3(64), 0, 0, x, y, reps); });
+        float t7 = timeit([&] { hipLaunchKernelGGL(mul_chain<7>, dim3(blk), dim3(64), 0, 0, x, y, reps); });
+        float t8 = timeit([&] { hipLaunchKernelGGL(mul_chain<8>, dim3(blk), dim3(64), 0, 0, x, y, reps); });
         double n = (double)blk * 64 * reps;
         printf("fe_mul waves %5d  V0 %7.1f ns/mul/wave %8.1f Gmul/s | V1 %7.1f ns %8.1f Gmul/s | V3 %7.1f ns %8.1f Gmul/s"
-               " | V4 %7.1f ns %8.1f Gmul/s | sqr5 %7.1f ns %8.1f Gsqr/s | V6 %7.1f ns %8.1f Gmul/s\n",
+               " | V4 %7.1f ns %8.1f Gmul/s | sqr5 %7.1f ns %8.1f Gsqr/s | V6 %7.1f ns %8.1f Gmul/s | V7 %7.1f ns %8.1f | V8 %7.1f ns %8.1f\n",
                blk, t0 * 1e6 / reps, n / t0 / 1e6, t1 * 1e6 / reps, n / t1 / 1e6, t3 * 1e6 / reps, n / t3 / 1e6,
-               t4 * 1e6 / reps, n / t4 / 1e6, t5 * 1e6 / reps, n / t5 / 1e6, t6 * 1e6 / reps, n / t6 / 1e6);
+               t4 * 1e6 / reps, n / t4 / 1e6, t5 * 1e6 / reps, n / t5 / 1e6, t6 * 1e6 / reps, n / t6 / 1e6, t7 * 1e6 / reps, n / t7 / 1e6,
+               t8 * 1e6 / reps, n / t8 / 1e6);
     }
     int r2 = 20000;
     for (int blk : {1, 1024, 16384}) {
