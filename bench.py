@@ -231,11 +231,19 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     stream = torch.cuda.current_stream()
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
-    per_round, ok_all, Ks, Ds, oks = [], True, [], [], []
+    per_round, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], True, [], [], [], [], []
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         seg, cs, csg = P.client_seed_table(m, nbrs, P.synthetic_pair_seed)
-        eng.client_mask_dev(seg, torch.from_numpy(cs).to(dev), csg, rows, L, stream=stream)
+        d_cs = torch.from_numpy(cs).to(dev)
+        eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=stream)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=stream)   # timed: all N clients' masked vectors
+        c1.record(stream)
+        torch.cuda.synchronize()
+        cm_ms.append(c0.elapsed_time(c1))
+        cm_words.append(int(seg[-1]) * L)
         n_off = int(round(dropout * N))
         off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, n_off, replace=False)) if n_off else \
             np.zeros(0, np.int64)
@@ -268,7 +276,11 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
-            "correct": ok_all, "checked_against_oracle": bool(check_oracle)}
+            "correct": ok_all, "checked_against_oracle": bool(check_oracle),
+            "client_masks": {"what": "all N clients' masked vectors y_i = 1 + PRG(m_i) +- PRG(s_ij) "
+                                     "(SA_ClientAgent.py:246-324), one flm_client_mask_dev launch",
+                             "ms": round(float(np.mean(cm_ms)), 4), "mask_words": int(np.mean(cm_words)),
+                             "G_words/s": round(float(np.mean(cm_words)) / float(np.mean(cm_ms)) / 1e6, 1)}}
 
 
 def measure_recovery(eng, torch, D, M, T, steps=10):

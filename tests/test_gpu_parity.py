@@ -289,3 +289,36 @@ def test_host_rows_pinned_and_pageable_mix(eng):
         want = O.aggregate_unmask(rows, seeds, signs, threads=8)
         assert np.array_equal(eng.aggregate_unmask(vecs, seeds, signs, L=L), want), (N, L)
         arena.free()
+
+
+def test_rows_beyond_2_32_elements(eng):
+    """16384 clients x 2^20 slots = 2^34 row elements (64 GiB in HBM): row offsets and the
+    planner's item table must be 64-bit.  Masked rows y_i = 1 + PRG(m_i) made on the GPU; the
+    server unmask of all m_i must give out == N in every slot."""
+    import torch
+    N, L = 16384, 1 << 20
+    g = rng(16384)
+    m = torch.from_numpy(g.integers(0, 256, size=(N, 32), dtype=np.uint8)).cuda()
+    rows = torch.empty((N, L), dtype=torch.int32, device="cuda")
+    eng.client_mask_dev(np.arange(N + 1, dtype=np.int64), m, np.ones(N, np.int8), rows, L)
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(rows, m, torch.full((N,), -1, dtype=torch.int8, device="cuda"), out, L=L)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().view(np.uint32)
+    assert np.all(o == N), np.flatnonzero(o != N)[:8]
+    # the last client's row, far past 2^32 elements, against the oracle
+    want = O.client_mask(np.array([0, 1], np.int64), m[N - 1:].cpu().numpy(), np.ones(1, np.int8), 2048)
+    assert np.array_equal(rows[N - 1, :2048].cpu().numpy().view(np.uint32), want[0])
+    del rows
+    torch.cuda.empty_cache()
+
+
+def test_counter_limit_2_36_slots(eng):
+    """Slots map to ChaCha blocks slot/16 with a 32-bit block counter: the last block below
+    2^36 slots is computed like the oracle's 64-bit counter; one slot further is an error."""
+    seed = bytes(range(32))
+    top = (1 << 36) - 16
+    got = eng.prg_expand([seed], 16, slot0=top)[0]
+    assert np.array_equal(got, O.prg(seed, 16, slot0=top))
+    with pytest.raises(RuntimeError):
+        eng.prg_expand([seed], 32, slot0=top)
