@@ -119,3 +119,19 @@ def test_pair_seed_pipeline_symmetric():
     assert seed(ai, Aj, 1) == seed(aj, Ai, 1)
     assert seed(ai, Aj, 1) == seed(ai, Aj, 2)
     assert seed(ai, Aj, 1) != seed(ai, C.mul(99), 1)
+
+
+def test_latency_model_matches_reference_golden():
+    """Pinned to the reference itself: tests/golden/latency.json was produced by importing the
+    reference's own model/LatencyModel.py (numpy-only, no shim; tests/golden/make_latency_golden.py).
+    Same parameters and RandomState seed -> the same latency for every call, in order."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "latency.json")) as f:
+        g = json.load(f)
+    calls = [tuple(c) for c in g["calls"]]
+    for name, c in g["cases"].items():
+        kw = {k: (np.array(v) if isinstance(v, list) else v) for k, v in c["kwargs"].items()}
+        m = LatencyModel(c["model"], random_state=np.random.RandomState(c["seed"]), kwargs=kw)
+        got = [float(m.get_latency(s, r)) for s, r in calls]
+        assert got == c["latencies"], name
