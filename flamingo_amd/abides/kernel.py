@@ -44,12 +44,16 @@ class Kernel:
 
     # ------------------------------------------------------------ queue
     def _push(self, when, recipient, mtype, msg):
-        heapq.heappush(self._events, (when, recipient, mtype.value, next(self._seq), mtype, msg))
+        # Kernel.py orders (time, (recipient, type, msg)): ties go to the lower recipient id, then
+        # MESSAGE before WAKEUP, then the message created first (Message.__lt__ on uniq), also
+        # when an event is re-queued for an agent that is in the future.
+        tie = msg.uniq if msg is not None else next(self._seq)
+        heapq.heappush(self._events, (when, recipient, mtype.value, tie, next(self._seq), mtype, msg))
 
     @property
     def messages(self):
         """Pending events as (time, (recipient, type, msg)) in delivery order (read-only view)."""
-        return [(e[0], (e[1], e[4], e[5])) for e in sorted(self._events)]
+        return [(e[0], (e[1], e[5], e[6])) for e in sorted(self._events)]
 
     # ----------------------------------------------------------- runner
     def runner(self, agents=(), startTime=None, stopTime=None, num_simulations=1, defaultComputationDelay=1,
@@ -79,7 +83,7 @@ class Kernel:
             wall0 = pd.Timestamp("now")
             handled = 0
             while self._events and self.currentTime is not None and self.currentTime <= self.stopTime:
-                when, recipient, _, _, mtype, msg = heapq.heappop(self._events)
+                when, recipient, _, _, _, mtype, msg = heapq.heappop(self._events)
                 self.currentTime = when
                 if handled % 100000 == 0:
                     print(f"\n--- Simulation time: {self.currentTime}, messages processed: {handled}, "

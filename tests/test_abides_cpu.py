@@ -135,3 +135,32 @@ def test_latency_model_matches_reference_golden():
         m = LatencyModel(c["model"], random_state=np.random.RandomState(c["seed"]), kwargs=kw)
         got = [float(m.get_latency(s, r)) for s, r in calls]
         assert got == c["latencies"], name
+
+
+def test_same_time_ties_follow_message_creation_order():
+    """Kernel.py queues (time, (recipient, type, msg)): equal delivery times go to the message
+    created first (Message.__lt__ on uniq), not the one sent first."""
+    log = []
+
+    class Sender(Agent):
+        def __init__(self, id):
+            super().__init__(id, "s", "Sender", np.random.RandomState(1))
+
+        def kernelStarting(self, startTime):
+            self.setComputationDelay(0)
+            super().kernelStarting(startTime)
+
+        def wakeup(self, t):
+            super().wakeup(t)
+            first, second = Message({"from": "first"}), Message({"from": "second"})
+            self.sendMessage(1, second)          # sent first, created second
+            self.sendMessage(1, first)
+
+    class Sink(Recorder):
+        def __init__(self):
+            super().__init__(1, [], log)
+
+    model = LatencyModel("deterministic", kwargs={"min_latency": 5})
+    run([Sender(0), Sink()], model)
+    got = [e[3] for e in log if e[0] == "msg"]
+    assert got == ["first", "second"]
