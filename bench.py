@@ -203,7 +203,8 @@ def main():
             res["other_configs"] = {
                 "c2": measure_config(eng, torch, P, "c2", N=128, L=16384, o=1, dropout=0.0, check_oracle=True),
                 "c3": measure_config(eng, torch, P, "c3", N=1024, L=1 << 18, o=2, dropout=0.0),
-                "c5": measure_config(eng, torch, P, "c5", N=4096, L=1 << 20, o=1, dropout=0.01, rounds=10),
+                "c5": measure_config(eng, torch, P, "c5", N=4096, L=1 << 20, o=1, dropout=0.01, rounds=10,
+                                     recovery=True),
             }
             c5 = res["other_configs"]["c5"]
             rec = measure_recovery(eng, torch, D=int(round(c5["dropout_pairs_D_mean"])),
@@ -222,19 +223,37 @@ def main():
     return 0 if ok else 1
 
 
-def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False):
+def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False, recovery=False):
     """One BASELINE config on this GPU: valid masked rows built on the GPU, `rounds` iterations
     (each its own neighbour graph and, with dropouts, its own offline set: PCG64(seed=iteration)),
-    `steps` timed device-resident rounds per iteration; out == |U| checked every iteration."""
+    `steps` timed device-resident rounds per iteration; out == |U| checked every iteration.
+
+    recovery=True: pair seeds are SHA-256 of group elements and the server gets m_i and s_ij only
+    as decryption shares (flamingo_amd.synthetic); the whole reconstruction_process -- GPU seed
+    recovery + unmask -- is also timed, sequential and with the recovery overlapped on a second
+    stream (flamingo_amd.reconstruct), each checked out == |U|."""
     dev = torch.device("cuda", torch.cuda.current_device())
     m = np.frombuffer(b"".join(P.bench_seed(name, i) for i in range(N)), np.uint8).reshape(N, 32)
     stream = torch.cuda.current_stream()
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
     per_round, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], True, [], [], [], [], []
+    rec_seq, rec_ovl, rec_ok = [], [], True
+    if recovery:
+        from flamingo_amd.reconstruct import ServerReconstruction
+        from flamingo_amd.synthetic import recovery_round
+        recon, point_cache = ServerReconstruction(eng, dev), {}
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
-        seg, cs, csg = P.client_seed_table(m, nbrs, P.synthetic_pair_seed)
+        n_off = int(round(dropout * N))
+        off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, n_off, replace=False)) if n_off else \
+            np.zeros(0, np.int64)
+        on = np.setdiff1d(np.arange(N), off)
+        if recovery:
+            R = recovery_round(eng, m, nbrs, on, off, T=20, committee=60, seed=it, point_cache=point_cache)
+            seg, cs, csg = R["seg"], R["client_seeds"], R["client_signs"]
+        else:
+            seg, cs, csg = P.client_seed_table(m, nbrs, P.synthetic_pair_seed)
         d_cs = torch.from_numpy(cs).to(dev)
         eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=stream)
         c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -244,11 +263,10 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         torch.cuda.synchronize()
         cm_ms.append(c0.elapsed_time(c1))
         cm_words.append(int(seg[-1]) * L)
-        n_off = int(round(dropout * N))
-        off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, n_off, replace=False)) if n_off else \
-            np.zeros(0, np.int64)
-        on = np.setdiff1d(np.arange(N), off)
-        ss, sg = P.server_seed_table(m, nbrs, on, off, P.synthetic_pair_seed)
+        if recovery:
+            ss, sg = R["server_seeds"], R["server_signs"]
+        else:
+            ss, sg = P.server_seed_table(m, nbrs, on, off, P.synthetic_pair_seed)
         r_on = rows if len(on) == N else rows[torch.from_numpy(on).to(dev)].contiguous()
         d_s, d_g = torch.from_numpy(ss).to(dev), torch.from_numpy(sg).to(dev)
         for _ in range(2):
@@ -267,12 +285,35 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             want = O.aggregate_unmask(r_on.cpu().numpy().view(np.uint32), ss, sg, threads=8)
             ok = ok and bool(np.array_equal(want, out.cpu().numpy().view(np.uint32)))
         ok_all &= ok
+        if recovery:
+            rt = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares",
+                                                              "pair_signs")}
+            for overlap, acc in ((False, rec_seq), (True, rec_ovl)):
+                args = (r_on, L, rt["lambdas"], rt["mi_shares"], rt["c1"], rt["pair_shares"], rt["pair_signs"], out)
+                recon.run(*args, stream=stream, overlap=overlap)
+                q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                q0.record(stream)
+                for _ in range(max(2, steps // 4)):
+                    recon.run(*args, stream=stream, overlap=overlap)
+                q1.record(stream)
+                torch.cuda.synchronize()
+                acc.append(q0.elapsed_time(q1) / max(2, steps // 4))
+                rec_ok &= bool(torch.all(out == len(on)).item())
         Ks.append(int(ss.shape[0]))
         Ds.append(int(ss.shape[0] - len(on)))
         oks.append(int(len(on)))
         del r_on
     ms = float(np.mean(per_round))
     nu = float(np.mean(oks))
+    extra = {}
+    if recovery:
+        extra["server_reconstruction"] = {
+            "what": "reconstruction_process from decryption shares: GPU m_i recovery (Shamir, mod n) + "
+                    "threshold-ElGamal combine + SHA-256 seed derivation + unmask (SA_ServiceAgent.py:499-605)",
+            "sequential_ms": round(float(np.mean(rec_seq)), 4),
+            "overlapped_ms": round(float(np.mean(rec_ovl)), 4),
+            "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
+            "schedule": "EC combine on a second stream under the self-mask unmask; pair masks in a second pass"}
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
@@ -280,7 +321,8 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "client_masks": {"what": "all N clients' masked vectors y_i = 1 + PRG(m_i) +- PRG(s_ij) "
                                      "(SA_ClientAgent.py:246-324), one flm_client_mask_dev launch",
                              "ms": round(float(np.mean(cm_ms)), 4), "mask_words": int(np.mean(cm_words)),
-                             "G_words/s": round(float(np.mean(cm_words)) / float(np.mean(cm_ms)) / 1e6, 1)}}
+                             "G_words/s": round(float(np.mean(cm_words)) / float(np.mean(cm_ms)) / 1e6, 1)},
+            **extra}
 
 
 def measure_recovery(eng, torch, D, M, T, steps=10):

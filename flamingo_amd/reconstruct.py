@@ -1,0 +1,82 @@
+"""Device-resident server reconstruction with seed recovery overlapped (one GPU).
+
+SA_ServiceAgent.reconstruction_process (:499-605) in order: recover every
+online client's m_i from the decryptors' Shamir shares (:506-526), recover
+every dropout pair's s_ij by threshold-ElGamal decryption (:542-585), then
+final_sum = S - sum PRG(m_i) + sum sigma PRG(s_ij) (:529-540, :587-605).
+
+Here the m_i recovery is tiny (flm_shamir_combine_dev, ~0.06 ms at c5) and
+unblocks the self-mask unmask of the row sum, the bulk of the VALU work.
+The EC combine (flm_ec_combine_dev) is latency-bound on ~300 waves, far from
+filling the chip, so it runs on a second HIP stream under that unmask.  The
+D pair masks are then added in a second pass over the one partial vector,
+seeds taken straight from the combine (no host round trip):
+
+  main stream:  shamir -> unmask(rows, m seeds)  -> tmp ---wait---> unmask(tmp, pair seeds) -> out
+  side stream:  ec_combine -> pair seeds --------------event--^
+
+`overlap=False` runs the same steps on one stream with a single unmask over all
+K seeds (the sequential schedule) for comparison.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class ServerReconstruction:
+    def __init__(self, engine, device=None):
+        self.eng = engine
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.side = torch.cuda.Stream(device=self.device)
+        self._bufs = {}
+
+    def _buf(self, name, shape, dtype, fill=None):
+        b = self._bufs.get(name)
+        if b is None or tuple(b.shape) != tuple(shape) or b.dtype != dtype:
+            b = torch.empty(shape, dtype=dtype, device=self.device)
+            if fill is not None:
+                b.fill_(fill)
+            self._bufs[name] = b
+        return b
+
+    def run(self, rows, L: int, lambdas, mi_shares, c1, pair_shares, pair_signs, out, stream=None,
+            overlap: bool = True):
+        """rows (N, pitch) int32; lambdas (T, 32), mi_shares (T, M, 32), c1 (D, 64), pair_shares
+        (T, D, 64) uint8; pair_signs (D,) int8; out (>= L,) int32 -- all CUDA tensors on this device.
+        Enqueues on `stream` (default: torch's current stream); returns (out, flags), flags (D,)
+        int32 from the combine (bits 0/1: a point was not on P-256, bit 2: result at infinity)."""
+        eng = self.eng
+        main = torch.cuda.current_stream(self.device) if stream is None else stream
+        M = mi_shares.shape[1]
+        D = c1.shape[0] if c1 is not None else 0
+        seeds = self._buf("seeds", (M + D, 32), torch.uint8)
+        flags = self._buf("flags", (max(D, 1),), torch.int32)
+        m_seeds, p_seeds = seeds[:M], seeds[M:]
+        if D == 0:
+            eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), out, L=L, stream=main)
+            return out, flags[:0]
+        if not overlap:
+            signs = self._buf("signs_all", (M + D,), torch.int8)
+            signs[:M].fill_(-1)
+            signs[M:].copy_(pair_signs)
+            eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+            eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=main)
+            eng.aggregate_unmask_dev(rows, seeds, signs, out, L=L, stream=main)
+            return out, flags
+        ready = torch.cuda.Event()
+        ready.record(main)                       # inputs enqueued on main are visible to the side stream
+        self.side.wait_event(ready)
+        eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+        pitch = rows.shape[1]
+        tmp = self._buf("tmp", (1, pitch), torch.int32)
+        eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), tmp[0], L=L, stream=main)
+        main.wait_event(done)
+        eng.aggregate_unmask_dev(tmp, p_seeds, pair_signs, out, L=L, stream=main)
+        # buffers used on the side stream must not be reused before it finishes
+        for t in (c1, pair_shares, lambdas, p_seeds, flags):
+            t.record_stream(self.side)
+        return out, flags
