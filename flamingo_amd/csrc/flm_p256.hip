@@ -462,6 +462,10 @@ __global__ __launch_bounds__(TPB) void ec_mul_kernel(const uint8_t *__restrict__
                                                      const uint8_t *__restrict__ scalars, int per_element, int T,
                                                      int D, uint32_t *__restrict__ jac,
                                                      uint32_t *__restrict__ flags) {
+    // Latency-bound (one wave's issue chain sets the time): when the unmask runs beside it on
+    // another stream (flamingo_amd/reconstruct.py), let these waves issue first; the
+    // throughput-bound unmask waves fill the remaining slots.
+    __builtin_amdgcn_s_setprio(3);
     const size_t g = (size_t)blockIdx.x * TPB + threadIdx.x;
     if (g >= (size_t)T * D) return;
     const int j = (int)(g / D);
@@ -504,6 +508,7 @@ __global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__
                                                                int negate, uint8_t *__restrict__ points_out,
                                                                uint8_t *__restrict__ digests_out,
                                                                uint32_t *__restrict__ flags) {
+    __builtin_amdgcn_s_setprio(3);
     const int i = blockIdx.x * kEcThreads + threadIdx.x;
     if (i >= D) return;
     uint32_t fl = 0;

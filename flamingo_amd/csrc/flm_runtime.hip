@@ -92,6 +92,7 @@ struct flm_ctx {
     int table_k = -1;  // seeds in the current device seed table
     int tune_variant = -1;   // items_kernel variant, -1 = auto
     int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
+    int tune_min_items = 1024;  // planner target for work items per aggregate launch
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
 };
@@ -230,11 +231,11 @@ void plan_job(const Job &j, uint64_t pitch, int subtiles, int parts_r, int parts
     }
 }
 
-int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t nseeds, int &pr, int &pm) {
+int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t nseeds, int &pr, int &pm,
+                 uint64_t kTarget = 1024) {
     // Balance mask units against row units, then split both until the grid
     // has a few workgroups per CU (16 waves each), keeping >= 16 rows/seeds
     // per item so every wave of a workgroup has work.
-    constexpr uint64_t kTarget = 1024;
     pr = 1;
     pm = 1;
     if (tiles_r && tiles_m && tiles_r > tiles_m) pm = (int)std::min<uint64_t>(nseeds, (tiles_r + tiles_m - 1) / tiles_m);
@@ -271,7 +272,8 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
 // and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
 // diagnostic entry point.
 void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo,
-                           uint64_t mask_hi, uint64_t prg_slot0, std::vector<Item> &items, Plan &plan) {
+                           uint64_t mask_hi, uint64_t prg_slot0, std::vector<Item> &items, Plan &plan,
+                           int min_items = 1024) {
     // ChaCha-heavy rounds keep 1024-slot tiles (16 waves split one tile's seeds);
     // row-streaming-heavy rounds (few seeds per slot) prefer 4 sub-tiles per
     // workgroup: 4096-slot tiles, fewer LDS combines (measured 5.77 vs 5.26 TB/s).
@@ -289,7 +291,7 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     const uint64_t tr = N > 0 ? (L + W - 1) / W : 0;
     const uint64_t tm = (K > 0 && mask_hi > mask_lo) ? (mask_hi - mask_lo + W - 1) / W : 0;
     int pr, pm;
-    choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm);
+    choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)min_items);
     plan.subtiles = subtiles;
     plan.seed_light = seed_light;
     plan_job(j, pitch, subtiles, pr, pm, pairing == 1, items, plan.needs_zero, plan.atomics, plan.single_tile);
@@ -297,14 +299,14 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
 
 Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
                      uint64_t prg_slot0, int *rc) {
-    PlanKey key{ctx->tune_subtiles + 100 * ctx->tune_pairing, pitch, (uint64_t)N, (uint64_t)K, L, mask_lo, mask_hi,
-                prg_slot0};
+    PlanKey key{ctx->tune_subtiles + 100 * ctx->tune_pairing + 1000 * ctx->tune_min_items, pitch, (uint64_t)N,
+                (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
     auto f = ctx->plans.find(key);
     if (f != ctx->plans.end()) { *rc = 0; return f->second; }
     std::vector<Item> items;
     Plan *plan = new Plan();
     build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items,
-                          *plan);
+                          *plan, ctx->tune_min_items);
     *rc = upload_plan(ctx, *plan, items);
     if (*rc) { plan->items.release(); delete plan; return nullptr; }
     if (ctx->plans.size() > 64) {  // bound the cache
@@ -800,6 +802,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
         if (value != 0 && value != 1 && value != 4 && value != 16)
             return fail(ctx, FLM_EINVAL, "subtiles must be 0 (auto), 1, 4 or 16");
         ctx->tune_subtiles = value;
+    } else if (k == "min_items") {
+        if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
+        ctx->tune_min_items = value;
     } else if (k == "ec_threads") {
         if (value != 64 && value != 128 && value != 256)
             return fail(ctx, FLM_EINVAL, "ec_threads must be 64, 128 or 256");

@@ -24,8 +24,9 @@ import torch
 
 
 class ServerReconstruction:
-    def __init__(self, engine, device=None):
+    def __init__(self, engine, device=None, pass1_min_items: int = 1024):
         self.eng = engine
+        self.pass1_min_items = pass1_min_items
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.side = torch.cuda.Stream(device=self.device)
         self._bufs = {}
@@ -73,7 +74,14 @@ class ServerReconstruction:
         eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
         pitch = rows.shape[1]
         tmp = self._buf("tmp", (1, pitch), torch.int32)
-        eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), tmp[0], L=L, stream=main)
+        if self.pass1_min_items != 1024:
+            eng.set_tuning("min_items", self.pass1_min_items)
+        try:
+            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), tmp[0], L=L,
+                                     stream=main)
+        finally:
+            if self.pass1_min_items != 1024:
+                eng.set_tuning("min_items", 1024)
         main.wait_event(done)
         eng.aggregate_unmask_dev(tmp, p_seeds, pair_signs, out, L=L, stream=main)
         # buffers used on the side stream must not be reused before it finishes

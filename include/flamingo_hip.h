@@ -146,6 +146,8 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              for aggregate plans.
  *   "pairing"  0 interleaved single-kind items | 1 dual-tile items (default), for
  *              windows where rows and masks cover different tiles.
+ *   "min_items" planner target for work items per aggregate launch
+ *              (default 1024; more items = finer load balance, more atomics).
  *   "ec_threads" 64 (default) | 128 | 256 lanes per workgroup of the P-256
  *              scalar-multiplication kernel. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
