@@ -223,6 +223,10 @@ def main():
     return 0 if ok else 1
 
 
+RECON_EC_CUS = 24        # CUs given to the EC combine in the CU-split schedule (tools/recon_probe.py sweep)
+RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
+
+
 def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False, recovery=False):
     """One BASELINE config on this GPU: valid masked rows built on the GPU, `rounds` iterations
     (each its own neighbour graph and, with dropouts, its own offline set: PCG64(seed=iteration)),
@@ -238,11 +242,13 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
     per_round, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], True, [], [], [], [], []
-    rec_seq, rec_ovl, rec_ok = [], [], True
+    rec_seq, rec_ovl, rec_cu, rec_ok = [], [], [], True
     if recovery:
         from flamingo_amd.reconstruct import ServerReconstruction
         from flamingo_amd.synthetic import recovery_round
         recon, point_cache = ServerReconstruction(eng, dev), {}
+        recon_cu = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=RECON_EC_CUS,
+                                        cu_pick="first")
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         n_off = int(round(dropout * N))
@@ -288,13 +294,14 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         if recovery:
             rt = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares",
                                                               "pair_signs")}
-            for overlap, acc in ((False, rec_seq), (True, rec_ovl)):
+            for rc, overlap, acc in ((recon, False, rec_seq), (recon, True, rec_ovl), (recon_cu, True, rec_cu)):
                 args = (r_on, L, rt["lambdas"], rt["mi_shares"], rt["c1"], rt["pair_shares"], rt["pair_signs"], out)
-                recon.run(*args, stream=stream, overlap=overlap)
+                out.fill_(0)
+                rc.run(*args, stream=stream, overlap=overlap)
                 q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 q0.record(stream)
                 for _ in range(max(2, steps // 4)):
-                    recon.run(*args, stream=stream, overlap=overlap)
+                    rc.run(*args, stream=stream, overlap=overlap)
                 q1.record(stream)
                 torch.cuda.synchronize()
                 acc.append(q0.elapsed_time(q1) / max(2, steps // 4))
@@ -312,8 +319,11 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
                     "threshold-ElGamal combine + SHA-256 seed derivation + unmask (SA_ServiceAgent.py:499-605)",
             "sequential_ms": round(float(np.mean(rec_seq)), 4),
             "overlapped_ms": round(float(np.mean(rec_ovl)), 4),
+            "cu_split_ms": round(float(np.mean(rec_cu)), 4),
             "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
-            "schedule": "EC combine on a second stream under the self-mask unmask; pair masks in a second pass"}
+            "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
+                        "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
+                        f"{RECON_EC_CUS} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS})"}
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),

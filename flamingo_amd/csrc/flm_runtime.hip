@@ -5,6 +5,7 @@
 // planner turns a round's shape into Items (flm_internal.h) so that every
 // workgroup carries an equal share of row streaming and mask generation.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -970,6 +971,39 @@ void *flm_host_alloc(size_t bytes) {
 
 void flm_host_free(void *p) {
     if (p) (void)hipHostFree(p);
+}
+
+int flm_cu_count(flm_ctx *ctx, int *n_cus) {
+    if (!ctx || !n_cus) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipDeviceGetAttribute(n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    return 0;
+}
+
+int flm_stream_create_cu_mask(flm_ctx *ctx, const uint32_t *mask, int n_words, void **stream_out) {
+    if (!ctx || !mask || !stream_out || n_words <= 0) return fail(ctx, FLM_EINVAL, "NULL argument or empty mask");
+    int n_cus = 0;
+    FLM_HIP(ctx, hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    int set = 0;
+    for (int w = 0; w < n_words; ++w)
+        for (int b = 0; b < 32; ++b)
+            if ((mask[w] >> b) & 1u) {
+                if (w * 32 + b >= n_cus)
+                    return fail(ctx, FLM_EINVAL, "CU mask names CU %d of %d", w * 32 + b, n_cus);
+                ++set;
+            }
+    if (set == 0) return fail(ctx, FLM_EINVAL, "CU mask selects no CU");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    FLM_HIP(ctx, hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
+    *stream_out = s;
+    return 0;
+}
+
+int flm_stream_destroy(flm_ctx *ctx, void *stream) {
+    if (!ctx || !stream) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_HIP(ctx, hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return 0;
 }
 
 }  // extern "C"

@@ -66,6 +66,9 @@ class MaskEngine:
     # ------------------------------------------------------------ plumbing
     def close(self):
         if getattr(self, "ctx", None) is not None and self.ctx.value:
+            for st in self.__dict__.pop("_cu_streams", {}).values():
+                st.synchronize()
+                self.lib.flm_stream_destroy(self.ctx, ctypes.c_void_p(st.cuda_stream))
             self.lib.flm_free(self.ctx)
             self.ctx = None
 
@@ -93,6 +96,32 @@ class MaskEngine:
         v = [ctypes.c_int() for _ in range(4)]
         self.lib.flm_last_plan(self.ctx, *[ctypes.byref(x) for x in v])
         return {"items": v[0].value, "tile_slots": v[1].value, "atomics": v[2].value, "variant": v[3].value}
+
+    def cu_count(self) -> int:
+        n = ctypes.c_int()
+        self._check(self.lib.flm_cu_count(self.ctx, ctypes.byref(n)), "flm_cu_count")
+        return n.value
+
+    def cu_stream(self, cus):
+        """A torch ExternalStream whose kernels run only on the logical CUs in `cus`
+        (flm_stream_create_cu_mask).  Cached per CU set and owned by the engine:
+        destroyed by close() after a device synchronize.  Never record_stream() a
+        tensor on it (the caching allocator would touch the stream after close)."""
+        import torch
+        cus = tuple(sorted(set(int(c) for c in cus)))
+        if not cus:
+            raise ValueError("cu_stream: empty CU set")
+        cache = self.__dict__.setdefault("_cu_streams", {})
+        if cus in cache:
+            return cache[cus]
+        words = np.zeros((max(cus) // 32) + 1, np.uint32)
+        for c in cus:
+            words[c // 32] |= np.uint32(1 << (c % 32))
+        h = ctypes.c_void_p()
+        self._check(self.lib.flm_stream_create_cu_mask(self.ctx, words.ctypes.data_as(ctypes.c_void_p), len(words),
+                                                        ctypes.byref(h)), "flm_stream_create_cu_mask")
+        cache[cus] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", self.device))
+        return cache[cus]
 
     # -------------------------------------------------------- host arrays
     def aggregate_unmask(self, vectors, seeds, signs, L: int | None = None) -> np.ndarray:

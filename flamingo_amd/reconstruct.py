@@ -17,6 +17,13 @@ seeds taken straight from the combine (no host round trip):
 
 `overlap=False` runs the same steps on one stream with a single unmask over all
 K seeds (the sequential schedule) for comparison.
+
+With `ec_cus > 0` the two streams are CU-partitioned (flm_stream_create_cu_mask):
+the combine runs on `ec_cus` CUs only and the Shamir step + self-mask unmask on
+the rest.  Unpartitioned, an EC wave resident on a SIMD leaves too few VGPRs for
+a second unmask workgroup on that CU, so those CUs run at half rate for the
+whole combine and finish last; partitioned, the unmask is evenly spread over
+the CUs it owns.  The pair pass then runs on the caller's stream over all CUs.
 """
 from __future__ import annotations
 
@@ -24,12 +31,29 @@ import torch
 
 
 class ServerReconstruction:
-    def __init__(self, engine, device=None, pass1_min_items: int = 1024):
+    def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride"):
         self.eng = engine
         self.pass1_min_items = pass1_min_items
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-        self.side = torch.cuda.Stream(device=self.device)
         self._bufs = {}
+        self._cu_streams = []
+        self.ec_cus = int(ec_cus)
+        self.part = None
+        if self.ec_cus > 0:
+            n = engine.cu_count()
+            if not 0 < self.ec_cus < n:
+                raise ValueError(f"ec_cus={ec_cus} must be in (0, {n})")
+            ec = pick_cus(n, self.ec_cus, cu_pick)
+            self.side = engine.cu_stream(ec)
+            self.part = engine.cu_stream([c for c in range(n) if c not in set(ec)])
+            self._cu_streams = [self.side, self.part]
+        else:
+            self.side = torch.cuda.Stream(device=self.device)
+
+    def close(self):
+        """The CU-partitioned streams belong to the engine (cached per CU set, destroyed
+        by MaskEngine.close()); nothing of ours outlives the last run's events."""
+        self._cu_streams = []
 
     def _buf(self, name, shape, dtype, fill=None):
         b = self._bufs.get(name)
@@ -71,6 +95,10 @@ class ServerReconstruction:
         eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
         done = torch.cuda.Event()
         done.record(self.side)
+        caller = main
+        if self.part is not None:
+            self.part.wait_event(ready)
+            main = self.part
         eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
         pitch = rows.shape[1]
         tmp = self._buf("tmp", (1, pitch), torch.int32)
@@ -82,9 +110,21 @@ class ServerReconstruction:
         finally:
             if self.pass1_min_items != 1024:
                 eng.set_tuning("min_items", 1024)
+        if main is not caller:
+            fin = torch.cuda.Event()
+            fin.record(main)
+            caller.wait_event(fin)
+            main = caller
+        # the caller's stream now waits for both streams' work, so every buffer they
+        # touched is safe to free or reuse in the caller's stream order (no
+        # record_stream, which would tie the allocator to a stream we may destroy)
         main.wait_event(done)
         eng.aggregate_unmask_dev(tmp, p_seeds, pair_signs, out, L=L, stream=main)
-        # buffers used on the side stream must not be reused before it finishes
-        for t in (c1, pair_shares, lambdas, p_seeds, flags):
-            t.record_stream(self.side)
         return out, flags
+
+
+def pick_cus(n: int, k: int, how: str = "stride"):
+    """k of n logical CU ids: evenly strided over the id space, or the first k."""
+    if how == "first":
+        return list(range(k))
+    return sorted({(i * n) // k for i in range(k)})

@@ -204,6 +204,18 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
  * (:397-400) products, n independent elements per call. */
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out);
 
+/* ------------------------------------------------ CU-partitioned streams */
+
+/* A HIP stream whose kernels run only on the CUs set in `mask` (n_words
+ * 32-bit words, bit i = logical CU i; hipExtStreamCreateWithCUMask).  The
+ * server reconstruction (SA_ServiceAgent.py:499-605) runs its latency-bound
+ * EC combine on a few CUs of one such stream while the VALU-bound self-mask
+ * unmask fills the complementary set on another, so neither evicts the other's
+ * workgroups.  *n_cus receives the device's CU count. */
+int flm_cu_count(flm_ctx *ctx, int *n_cus);
+int flm_stream_create_cu_mask(flm_ctx *ctx, const uint32_t *mask, int n_words, void **stream_out);
+int flm_stream_destroy(flm_ctx *ctx, void *stream);
+
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */
 void *flm_host_alloc(size_t bytes);

@@ -27,8 +27,10 @@ del rows
 t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
-for overlap, mi in ((False, 1024), (True, 1024), (True, 4096), (True, 16384)):
-    rec = ServerReconstruction(eng, pass1_min_items=mi)
+cases = [(False, 1024, 0, "stride"), (True, 1024, 0, "stride")]
+cases += [(True, 1024, k, "first") for k in (24, 32, 40, 48)] + [(True, 4096, k, "first") for k in (24, 32, 40)]
+for overlap, mi, ec_cus, pick in cases:
+    rec = ServerReconstruction(eng, pass1_min_items=mi, ec_cus=ec_cus, cu_pick=pick)
     with torch.cuda.stream(main):
         for _ in range(2):
             rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out,
@@ -40,5 +42,6 @@ for overlap, mi in ((False, 1024), (True, 1024), (True, 4096), (True, 16384)):
                     stream=main, overlap=overlap)
         e1.record(main)
     torch.cuda.synchronize()
-    print(f"overlap={overlap} min_items={mi} ms={e0.elapsed_time(e1) / 5:.3f} correct={bool(torch.all(out == len(on)).item())}",
+    rec.close()
+    print(f"overlap={overlap} min_items={mi} ec_cus={ec_cus} pick={pick} ms={e0.elapsed_time(e1) / 5:.3f} correct={bool(torch.all(out == len(on)).item())}",
           flush=True)
