@@ -241,7 +241,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     stream = torch.cuda.current_stream()
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
-    per_round, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], True, [], [], [], [], []
+    per_round, per_round_graph, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], [], True, [], [], [], [], []
     rec_seq, rec_ovl, rec_cu, rec_ok = [], [], [], True
     if recovery:
         from flamingo_amd.reconstruct import ServerReconstruction
@@ -285,6 +285,19 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         torch.cuda.synchronize()
         per_round.append(e0.elapsed_time(e1) / steps)
         ok = bool(torch.all(out == len(on)).item())
+        # the same round captured once as a HIP graph, replayed with one launch per round
+        rg = eng.round_graph(r_on, d_s, d_g, out, L=L)
+        out.fill_(0)
+        rg.launch(stream)
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        for _ in range(steps):
+            rg.launch(stream)
+        g1.record(stream)
+        torch.cuda.synchronize()
+        per_round_graph.append(g0.elapsed_time(g1) / steps)
+        ok = ok and bool(torch.all(out == len(on)).item())
+        rg.close()
         if check_oracle:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # checker only
@@ -311,6 +324,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         oks.append(int(len(on)))
         del r_on
     ms = float(np.mean(per_round))
+    msg = float(np.mean(per_round_graph))
     nu = float(np.mean(oks))
     extra = {}
     if recovery:
@@ -327,6 +341,9 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
+            "graph": {"what": "the same round captured as a HIP graph (flm_round_graph_create), one "
+                              "hipGraphLaunch per round", "ms_per_round": round(msg, 4),
+                      "GB/s": round((4.0 * nu * L + 4.0 * L) / (msg * 1e-3) / 1e9, 1)},
             "correct": ok_all, "checked_against_oracle": bool(check_oracle),
             "client_masks": {"what": "all N clients' masked vectors y_i = 1 + PRG(m_i) +- PRG(s_ij) "
                                      "(SA_ClientAgent.py:246-324), one flm_client_mask_dev launch",
@@ -480,7 +497,8 @@ def with_copy(eng, torch, rows, seeds, signs, L, n_online):
     arena.free()
     best = min(t)
     return {"ms_per_round": round(best * 1e3, 2), "GB/s": round((4.0 * N * L + 4.0 * L) / best / 1e9, 2),
-            "correct": ok, "path": "flm_aggregate_unmask: per-row hipMemcpyAsync from pinned host + D2H of out"}
+            "correct": ok, "path": "flm_aggregate_unmask: pinned host rows, host-contiguous runs of <=16 rows per "
+                    "hipMemcpyAsync over 4 copy streams, + D2H of out"}
 
 
 def cpu_baseline(rows, seeds, signs, L, gpu_out):

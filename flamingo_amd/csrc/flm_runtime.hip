@@ -26,6 +26,7 @@ using flm::SeedRec;
 namespace {
 
 thread_local std::string g_last_error;
+constexpr int kCopyStreams = 4;
 
 struct DevBuf {
     void *p = nullptr;
@@ -87,6 +88,10 @@ struct flm_ctx {
     void *stage[2] = {nullptr, nullptr};
     size_t stage_cap = 0;
     hipEvent_t stage_done[2] = {nullptr, nullptr};
+    // host->device streams for page-locked rows (several SDMA engines)
+    hipStream_t copy[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t copy_done[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t copy_start = nullptr;
     std::map<PlanKey, Plan *> plans;
     Plan scratch_plan;  // uncached plans (client masking, expansion)
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
@@ -380,13 +385,42 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
     uint32_t *dst = ctx->rows.as<uint32_t>();
     const size_t row_bytes = L * sizeof(uint32_t);
     const size_t slot_bytes = pitch * sizeof(uint32_t);
-    std::vector<int> pageable;
+    std::vector<int> pageable, pinned;
     for (int i = 0; i < N; ++i) {
         if (!rows[i]) return fail(ctx, FLM_EINVAL, "row %d is NULL", i);
-        if (host_pinned(rows[i]))
-            FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)i * pitch, rows[i], row_bytes, hipMemcpyHostToDevice, ctx->stream));
-        else
-            pageable.push_back(i);
+        (host_pinned(rows[i]) ? pinned : pageable).push_back(i);
+    }
+    if (!pinned.empty()) {
+        // Page-locked rows go straight to the device, spread over kCopyStreams
+        // streams (several SDMA engines: one stream tops out near 49 GB/s, four
+        // reach the link's ~57 GB/s, tools/h2d_probe.hip).  Runs of rows that are
+        // contiguous on the host (an arena) move as one copy of up to 16 rows.
+        if (!ctx->copy[0]) {
+            for (int c = 0; c < kCopyStreams; ++c) {
+                FLM_HIP(ctx, hipStreamCreateWithFlags(&ctx->copy[c], hipStreamNonBlocking));
+                FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->copy_done[c], hipEventDisableTiming));
+            }
+            FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->copy_start, hipEventDisableTiming));
+        }
+        // the row buffer may still be read by the previous round on ctx->stream
+        FLM_HIP(ctx, hipEventRecord(ctx->copy_start, ctx->stream));
+        for (int c = 0; c < kCopyStreams; ++c) FLM_HIP(ctx, hipStreamWaitEvent(ctx->copy[c], ctx->copy_start, 0));
+        int next = 0;
+        for (size_t k = 0; k < pinned.size();) {
+            const int first = pinned[k];
+            size_t n = 1;
+            while (pitch == L && n < 16 && k + n < pinned.size() && pinned[k + n] == first + (int)n &&
+                   rows[first + n] == rows[first] + n * L)
+                ++n;
+            FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)first * pitch, rows[first], (n - 1) * slot_bytes + row_bytes,
+                                        hipMemcpyHostToDevice, ctx->copy[next]));
+            next = (next + 1) % kCopyStreams;
+            k += n;
+        }
+        for (int c = 0; c < kCopyStreams; ++c) {
+            FLM_HIP(ctx, hipEventRecord(ctx->copy_done[c], ctx->copy[c]));
+            FLM_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->copy_done[c], 0));
+        }
     }
     if (pageable.empty()) return 0;
     if (slot_bytes > kStageBytes) {  // very long rows: one DMA per row through HIP's own staging
@@ -552,6 +586,12 @@ void flm_free(flm_ctx *ctx) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
         if (ctx->stage_done[i]) (void)hipEventDestroy(ctx->stage_done[i]);
     }
+    for (int c = 0; c < 4; ++c) {
+        if (ctx->copy[c]) (void)hipStreamSynchronize(ctx->copy[c]);
+        if (ctx->copy[c]) (void)hipStreamDestroy(ctx->copy[c]);
+        if (ctx->copy_done[c]) (void)hipEventDestroy(ctx->copy_done[c]);
+    }
+    if (ctx->copy_start) (void)hipEventDestroy(ctx->copy_start);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -630,6 +670,92 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
     if (int rc = flm_seed_table_dev(ctx, d_seeds, d_signs, K, stream)) return rc;
     return flm_aggregate_dev(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out, stream);
+}
+
+// A whole device-resident round captured once as a HIP graph: seed schedule,
+// zero-fill (when the plan uses atomics) and the items launch replay with one
+// hipGraphLaunch.  The graph owns its plan, seed table and meta buffers, so the
+// context's caches may be evicted or regrown while it lives; the caller keeps
+// rows/seeds/signs/out alive and may rewrite their contents between launches.
+struct flm_round_graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    DevBuf recs, meta;
+    Plan plan;
+    void destroy() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        if (graph) (void)hipGraphDestroy(graph);
+        exec = nullptr;
+        graph = nullptr;
+        recs.release();
+        meta.release();
+        plan.items.release();
+    }
+};
+
+int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
+                           const int8_t *d_signs, int K, size_t L, size_t mask_lo, size_t mask_hi, uint64_t prg_slot0,
+                           uint32_t *d_out, void **graph_out) {
+    if (!ctx || !graph_out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    *graph_out = nullptr;
+    if (L == 0) return fail(ctx, FLM_EINVAL, "L must be > 0");
+    if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
+    if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    auto *g = new flm_round_graph();
+    hipStream_t cs = nullptr;
+    bool capturing = false;
+    auto bail = [&](int code) {
+        if (capturing) {
+            hipGraph_t junk = nullptr;
+            (void)hipStreamEndCapture(cs, &junk);
+            if (junk) (void)hipGraphDestroy(junk);
+        }
+        if (cs) (void)hipStreamDestroy(cs);
+        g->destroy();
+        delete g;
+        return code;
+    };
+    std::vector<Item> items;
+    build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0,
+                          items, g->plan, ctx->tune_min_items);
+    if (int rc = upload_plan(ctx, g->plan, items)) return bail(rc);
+    hipError_t e = g->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec));
+    if (e == hipSuccess) e = g->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)((std::max(K, 1) + 255) / 256)));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    capturing = e == hipSuccess;
+    if (e == hipSuccess)
+        e = flm::launch_seed_schedule(d_seeds, d_signs, K, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), cs);
+    if (e == hipSuccess && g->plan.needs_zero) e = hipMemsetAsync(d_out, 0, L * sizeof(uint32_t), cs);
+    if (e == hipSuccess)
+        e = flm::launch_items(g->plan.subtiles, pick_variant(ctx, g->plan), g->plan.items.as<Item>(), g->plan.n_items,
+                              d_rows, row_pitch, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), d_out, cs);
+    if (e == hipSuccess) {
+        capturing = false;
+        e = hipStreamEndCapture(cs, &g->graph);
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) return bail(fail(ctx, FLM_EHIP, "round graph capture: %s", hipGetErrorString(e)));
+    (void)hipStreamDestroy(cs);
+    *graph_out = g;
+    return 0;
+}
+
+int flm_round_graph_launch(flm_ctx *ctx, void *graph, void *stream) {
+    if (!ctx || !graph) return fail(ctx, FLM_EINVAL, "NULL argument");
+    auto *g = static_cast<flm_round_graph *>(graph);
+    FLM_HIP(ctx, hipGraphLaunch(g->exec, static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int flm_round_graph_destroy(flm_ctx *ctx, void *graph) {
+    if (!ctx || !graph) return fail(ctx, FLM_EINVAL, "NULL argument");
+    auto *g = static_cast<flm_round_graph *>(graph);
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    g->destroy();
+    delete g;
+    return 0;
 }
 
 int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,

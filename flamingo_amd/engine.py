@@ -235,6 +235,23 @@ class MaskEngine:
         self._check(rc, "flm_aggregate_unmask_dev")
         return out
 
+    def round_graph(self, rows, seeds, signs, out, L: int | None = None, mask_lo: int = 0,
+                    mask_hi: int | None = None, prg_slot0: int = 0) -> "RoundGraph":
+        """Capture aggregate_unmask_dev's round as a HIP graph (flm_round_graph_create): one
+        hipGraphLaunch per replay.  The tensors are kept alive by the returned object."""
+        N = rows.shape[0] if rows is not None else 0
+        pitch = rows.shape[1] if N else 0
+        L = pitch if L is None else L
+        mask_hi = L if mask_hi is None else mask_hi
+        K = seeds.shape[0] if seeds is not None else 0
+        h = ctypes.c_void_p()
+        rc = self.lib.flm_round_graph_create(
+            self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N,
+            ctypes.c_void_p(seeds.data_ptr() if K else 0), ctypes.c_void_p(signs.data_ptr() if K else 0), K, L,
+            mask_lo, mask_hi, prg_slot0, ctypes.c_void_p(out.data_ptr()), ctypes.byref(h))
+        self._check(rc, "flm_round_graph_create")
+        return RoundGraph(self, h, (rows, seeds, signs, out))
+
     def seed_table_dev(self, seeds, signs, stream=None):
         """Build the device seed schedule (first of the round's two launches)."""
         K = seeds.shape[0] if seeds is not None else 0
@@ -390,6 +407,29 @@ class MaskEngine:
         bad = ctypes.c_int()
         self._check(self.lib.flm_check_signs(self.ctx, ctypes.byref(bad)), "flm_check_signs")
         return bad.value
+
+
+class RoundGraph:
+    """A captured device-resident round (see MaskEngine.round_graph)."""
+
+    def __init__(self, eng: MaskEngine, handle, keep):
+        self.eng, self.h, self._keep = eng, handle, keep
+
+    def launch(self, stream=None):
+        self.eng._check(self.eng.lib.flm_round_graph_launch(self.eng.ctx, self.h, self.eng._stream_handle(stream)),
+                        "flm_round_graph_launch")
+        return self._keep[3]
+
+    def close(self):
+        if self.h is not None and self.h.value and self.eng.ctx is not None:
+            self.eng._check(self.eng.lib.flm_round_graph_destroy(self.eng.ctx, self.h), "flm_round_graph_destroy")
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class PinnedArena:

@@ -204,6 +204,21 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
  * (:397-400) products, n independent elements per call. */
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out);
 
+/* ------------------------------------------------------ captured rounds */
+
+/* One device-resident round (flm_aggregate_unmask_dev's seed schedule,
+ * zero-fill and aggregate launch) captured as a HIP graph and replayed with a
+ * single hipGraphLaunch: the launch-bound small rounds (BASELINE c2, N=128,
+ * L=16384) pay one submission instead of three.  Arguments as
+ * flm_aggregate_unmask_dev; the pointers are baked into the graph, so the
+ * caller keeps those buffers alive (contents may change between launches).
+ * The graph owns its plan and seed table; flm_check_signs does not see it. */
+int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
+                           const int8_t *d_signs, int K, size_t L, size_t mask_lo, size_t mask_hi, uint64_t prg_slot0,
+                           uint32_t *d_out, void **graph_out);
+int flm_round_graph_launch(flm_ctx *ctx, void *graph, void *stream);
+int flm_round_graph_destroy(flm_ctx *ctx, void *graph);
+
 /* ------------------------------------------------ CU-partitioned streams */
 
 /* A HIP stream whose kernels run only on the CUs set in `mask` (n_words
