@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--variants", default="coalesced,block,merged,merged_w8")
     ap.add_argument("--subtiles", default="1,4")
     ap.add_argument("--pairing", default="0")
+    ap.add_argument("--min-items", default="1024")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     eng = MaskEngine(0)
@@ -43,20 +44,21 @@ def main():
     torch.cuda.set_stream(s)
     res = []
     for wl in args.workloads.split(","):
-        K = {"full": 1024, "pairs": 204, "shard8": 8192}[wl]
+        K = {"full": 1024, "pairs": 204, "shard8": 8192, "rows": 0}[wl]
         lo, hi = (0, L) if wl != "shard8" else (3 * L // 8, 4 * L // 8)
-        seeds = torch.randint(0, 256, (K, 32), dtype=torch.uint8, device="cuda", generator=g)
-        signs = (torch.randint(0, 2, (K,), device="cuda", generator=g) * 2 - 1).to(torch.int8)
+        seeds = torch.randint(0, 256, (max(K, 1), 32), dtype=torch.uint8, device="cuda", generator=g)[:K]
+        signs = (torch.randint(0, 2, (max(K, 1),), device="cuda", generator=g) * 2 - 1).to(torch.int8)[:K]
         eng.seed_table_dev(seeds, signs, stream=s)
-        times = {}
+        times, plans = {}, {}
         ref = None
-        combos = [(v, st, pa) for v in args.variants.split(",") for st in map(int, args.subtiles.split(","))
-                  for pa in map(int, args.pairing.split(","))]
+        combos = [(v, st, pa, mi) for v in args.variants.split(",") for st in map(int, args.subtiles.split(","))
+                  for pa in map(int, args.pairing.split(",")) for mi in map(int, args.min_items.split(","))]
         for rnd in range(args.rounds):
-            for v, st, pa in combos:
+            for v, st, pa, mi in combos:
                 eng.set_tuning("variant", VARIANTS[v])
                 eng.set_tuning("subtiles", st)
                 eng.set_tuning("pairing", pa)
+                eng.set_tuning("min_items", mi)
                 eng.aggregate_dev(rows, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=s)  # warm / plan
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
                 e[0].record(s)
@@ -65,17 +67,18 @@ def main():
                     e[r + 1].record(s)
                 torch.cuda.synchronize()
                 ms = [e[i].elapsed_time(e[i + 1]) for i in range(args.reps)]
-                times.setdefault((v, st, pa), []).extend(ms)
+                times.setdefault((v, st, pa, mi), []).extend(ms)
                 o = out.cpu().numpy()
                 if ref is None:
                     ref = o.copy()
                 elif not np.array_equal(ref, o):
-                    print(f"MISMATCH {wl} {v} st={st} pairing={pa}", flush=True)
-                plan = eng.last_plan()
-        for (v, st, pa), ms in times.items():
+                    print(f"MISMATCH {wl} {v} st={st} pairing={pa} min_items={mi}", flush=True)
+                plans[(v, st, pa, mi)] = eng.last_plan()
+        for (v, st, pa, mi), ms in times.items():
             med, mn = float(np.median(ms)), float(np.min(ms))
             gbs = (4.0 * N * L + 4.0 * L) / (med * 1e-3) / 1e9
-            r = {"workload": wl, "variant": v, "subtiles": st, "pairing": pa, "median_ms": round(med, 4), "min_ms": round(mn, 4),
+            r = {"workload": wl, "variant": v, "subtiles": st, "pairing": pa, "min_items": mi,
+                 "items": plans[(v, st, pa, mi)]["items"], "median_ms": round(med, 4), "min_ms": round(mn, 4),
                  "GB/s": round(gbs, 1)}
             res.append(r)
             print(json.dumps(r), flush=True)
