@@ -28,7 +28,7 @@ t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
 cases = [(False, 1024, 0, "stride"), (True, 1024, 0, "stride")]
-cases += [(True, 1024, k, "first") for k in (24, 32, 40, 48)] + [(True, 4096, k, "first") for k in (24, 32, 40)]
+cases += [(True, mi, k, "first") for k in (16, 24, 32, 40) for mi in (4096, 16384)]
 for overlap, mi, ec_cus, pick in cases:
     rec = ServerReconstruction(eng, pass1_min_items=mi, ec_cus=ec_cus, cu_pick=pick)
     with torch.cuda.stream(main):
