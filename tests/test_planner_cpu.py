@@ -108,3 +108,16 @@ def test_plan_modes():
     assert f & 8 and (f >> 8) == 4                         # seed-light: 4096-slot tiles
     _, f, _ = plan(1024, 8192, 1 << 20, 0, 1 << 17)
     assert f & 2 and f & 1 and not f & 4                   # shard: dual-tile, atomics
+
+
+def test_pick_cus_balances_xcds():
+    """ServerReconstruction's EC CU set: CU-mask bit i selects XCD i % 8 (profiles/r01_cu_map_probe.log),
+    so "first k" takes k/8 CUs from every XCD; the complement is what the unmask runs on."""
+    from flamingo_amd.reconstruct import pick_cus
+    for k in (8, 16, 24, 32):
+        ec = pick_cus(256, k, "first")
+        assert len(ec) == k and len(set(ec)) == k
+        per_xcd = np.bincount(np.array(ec) % 8, minlength=8)
+        assert per_xcd.min() == per_xcd.max() == k // 8
+    st = pick_cus(256, 24, "stride")
+    assert len(st) == 24 and max(st) < 256
