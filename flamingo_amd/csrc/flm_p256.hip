@@ -293,7 +293,7 @@ __device__ __forceinline__ Jac jac_dbl(const Jac &P) {
 }
 
 // add-2007-bl with the exceptional cases (P == Q, P == -Q, infinity) handled
-__device__ Jac jac_add(const Jac &P, const Jac &Q) {
+__device__ __forceinline__ Jac jac_add(const Jac &P, const Jac &Q) {
     if (fe_is_zero(P.Z)) return Q;
     if (fe_is_zero(Q.Z)) return P;
     Fe z1z1 = fe_sqr(P.Z);
@@ -452,13 +452,62 @@ __device__ __forceinline__ Jac load_jac(const uint32_t *jac, size_t plane_stride
     return R;
 }
 
+// Width-5 NAF of a 256-bit scalar (32-byte big endian) into d[0..kNafLen), least significant
+// digit first: digits are 0 or odd in [-15, 15] and every non-zero digit is followed by at
+// least four zeros, so a scalar multiplication costs ~256/6 additions instead of 64 (4-bit
+// windows).  A ninth limb absorbs k + 15 for scalars near 2^256.
+constexpr int kNafLen = 258;
+
+__device__ __forceinline__ void wnaf5(const uint8_t *k_be, int8_t (&d)[kNafLen]) {
+    uint32_t k[9];
+    {
+        const Fe f = load_be(k_be);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) k[i] = f.v[i];
+        k[8] = 0;
+    }
+#pragma unroll 1
+    for (int i = 0; i < kNafLen; ++i) {
+        int v = 0;
+        if (k[0] & 1u) {
+            v = (int)(k[0] & 31u);
+            if (v >= 16) v -= 32;
+            // k -= v  (v odd, |v| <= 15)
+            uint64_t c;
+            if (v > 0) {
+                c = (uint64_t)k[0] - (uint32_t)v;
+                k[0] = (uint32_t)c;
+#pragma unroll
+                for (int l = 1; l < 9; ++l) {
+                    c = (uint64_t)k[l] - (c >> 63);
+                    k[l] = (uint32_t)c;
+                }
+            } else {
+                c = (uint64_t)k[0] + (uint32_t)(-v);
+                k[0] = (uint32_t)c;
+#pragma unroll
+                for (int l = 1; l < 9; ++l) {
+                    c = (uint64_t)k[l] + (c >> 32);
+                    k[l] = (uint32_t)c;
+                }
+            }
+        }
+        d[i] = (int8_t)v;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) k[l] = (k[l] >> 1) | (k[l + 1] << 31);
+        k[8] >>= 1;
+    }
+}
+
 // Scalar multiplication scalar * point for T x D (term, element) pairs, flattened to one lane
 // per pair g = j*D + i (1-D grid; the workgroup size is a launch parameter).
 // points: [T][D][64] wire bytes; scalars: [T][32] (one per term) or [T][D][32] when
 // per_element; jac out: SoA planes [T][24][D].
-// Fixed 4-bit windows from the most significant nibble; 4 doublings + 1 add per window.
-template <int TPB>
-__global__ __launch_bounds__(TPB) void ec_mul_kernel(const uint8_t *__restrict__ points,
+// wNAF (w = 5) with a table of the odd multiples P, 3P, ..., 15P: ~256 doublings and ~43
+// additions from the most significant digit (was: fixed 4-bit windows, 252 + 63 + 13 table).
+// The combine's scalars are one per term, so a wave's digits (and branches) are uniform.
+template <int TPB, int WPE>
+__global__ __launch_bounds__(TPB, WPE) void ec_mul_kernel(const uint8_t *__restrict__ points,
                                                      const uint8_t *__restrict__ scalars, int per_element, int T,
                                                      int D, uint32_t *__restrict__ jac,
                                                      uint32_t *__restrict__ flags) {
@@ -474,27 +523,27 @@ __global__ __launch_bounds__(TPB) void ec_mul_kernel(const uint8_t *__restrict__
     Jac P;
     bool ok = load_point(points + e * 64, P);
     if (!ok) atomicOr(&flags[i], 2u);
-    const uint8_t *k = scalars + (per_element ? e : (size_t)j) * 32;
+    int8_t dig[kNafLen];
+    wnaf5(scalars + (per_element ? e : (size_t)j) * 32, dig);
 
-    Jac tab[16];
-    tab[0] = jac_inf();
-    tab[1] = P;
-    tab[2] = jac_dbl(P);
+    Jac tab[8];  // tab[t] = (2t+1) P
+    tab[0] = P;
+    const Jac P2 = jac_dbl(P);
 #pragma unroll 1
-    for (int t = 3; t < 16; ++t) tab[t] = jac_add(tab[t - 1], P);
+    for (int t = 1; t < 8; ++t) tab[t] = jac_add(tab[t - 1], P2);
 
-    Jac acc = tab[k[0] >> 4];
+    Jac acc = jac_inf();
+    bool started = false;
 #pragma unroll 1
-    for (int w = 1; w < 64; ++w) {
-        if (!fe_is_zero(acc.Z)) {
-            acc = jac_dbl(acc);
-            acc = jac_dbl(acc);
-            acc = jac_dbl(acc);
-            acc = jac_dbl(acc);
+    for (int w = kNafLen - 1; w >= 0; --w) {
+        if (started) acc = jac_dbl(acc);
+        const int v = dig[w];
+        if (v) {
+            Jac Q = tab[(v < 0 ? -v : v) >> 1];
+            if (v < 0) Q.Y = fe_neg(Q.Y);
+            acc = started ? jac_add(acc, Q) : Q;
+            started = true;
         }
-        uint32_t byte = k[w >> 1];
-        uint32_t d = (w & 1) ? (byte & 15u) : (byte >> 4);
-        if (d) acc = jac_add(acc, tab[d]);
     }
     if (!ok) acc = jac_inf();
     store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
@@ -630,24 +679,31 @@ __global__ __launch_bounds__(kEcThreads) void shamir_combine_kernel(const uint8_
 
 }  // namespace
 
-hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
-                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads) {
-    if (T <= 0 || D <= 0) return hipSuccess;
+template <int TPB, int WPE>
+static void launch_ec_mul_t(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
+                            uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream) {
     const size_t n = (size_t)T * D;
-    switch (threads) {
-        case 64:
-            hipLaunchKernelGGL(ec_mul_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, stream, d_points,
-                               d_scalars, per_element, T, D, d_jac, d_flags);
-            break;
-        case 128:
-            hipLaunchKernelGGL(ec_mul_kernel<128>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, stream, d_points,
-                               d_scalars, per_element, T, D, d_jac, d_flags);
-            break;
-        default:
-            hipLaunchKernelGGL(ec_mul_kernel<256>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, d_points,
-                               d_scalars, per_element, T, D, d_jac, d_flags);
-            break;
+    hipLaunchKernelGGL((ec_mul_kernel<TPB, WPE>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, stream,
+                       d_points, d_scalars, per_element, T, D, d_jac, d_flags);
+}
+
+// threads: lanes per workgroup (64/128/256); waves: register budget, as minimum waves per SIMD
+// (2: no cap, 172 VGPRs; 4: 128 VGPRs; 8: 64 VGPRs, both with spills)
+hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves) {
+    if (T <= 0 || D <= 0) return hipSuccess;
+#define FLM_EC(TPB)                                                                                          \
+    switch (waves) {                                                                                         \
+        case 4: launch_ec_mul_t<TPB, 4>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
+        case 8: launch_ec_mul_t<TPB, 8>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
+        default: launch_ec_mul_t<TPB, 1>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
     }
+    switch (threads) {
+        case 64: FLM_EC(64) break;
+        case 128: FLM_EC(128) break;
+        default: FLM_EC(256) break;
+    }
+#undef FLM_EC
     return hipGetLastError();
 }
 

@@ -100,6 +100,7 @@ struct flm_ctx {
     int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
     int tune_min_items = 1024;  // planner target for work items per aggregate launch
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
+    int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
 };
 
@@ -929,6 +930,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
         if (value != 0 && value != 1 && value != 4 && value != 16)
             return fail(ctx, FLM_EINVAL, "subtiles must be 0 (auto), 1, 4 or 16");
         ctx->tune_subtiles = value;
+    } else if (k == "ec_waves") {
+        if (value != 1 && value != 4 && value != 8) return fail(ctx, FLM_EINVAL, "ec_waves must be 1, 4 or 8");
+        ctx->tune_ec_waves = value;
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;
@@ -982,7 +986,7 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
-                                    ctx->tune_ec_threads));
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves));
     FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), T, D, negate, d_points_out, d_seeds_out,
                                        d_flags, s));
     return 0;
@@ -1076,7 +1080,7 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     FLM_HIP(ctx, hipMemsetAsync(ctx->ec_flags.p, 0, (size_t)n * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), 1, 1, n,
                                     ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s,
-                                    ctx->tune_ec_threads));
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves));
     FLM_HIP(ctx, flm::launch_ec_finish(nullptr, ctx->ec_jac.as<uint32_t>(), 1, n, 0, ctx->ec_out.as<uint8_t>(),
                                        nullptr, ctx->ec_flags.as<uint32_t>(), s));
     std::vector<uint32_t> fl(n);

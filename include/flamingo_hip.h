@@ -149,7 +149,9 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "min_items" planner target for work items per aggregate launch
  *              (default 1024; more items = finer load balance, more atomics).
  *   "ec_threads" 64 (default) | 128 | 256 lanes per workgroup of the P-256
- *              scalar-multiplication kernel. */
+ *              scalar-multiplication kernel.
+ *   "ec_waves" 1 (default: uncapped registers) | 4 | 8 minimum waves per SIMD the
+ *              scalar-multiplication kernel is compiled for (more waves, more spills). */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the

@@ -27,9 +27,18 @@ del rows
 t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
-cases = [(False, 1024, 0, "stride"), (True, 1024, 0, "stride")]
-cases += [(True, mi, k, "first") for k in (16, 24, 32, 40) for mi in (4096, 16384)]
-for overlap, mi, ec_cus, pick in cases:
+import bench  # noqa: E402
+
+EC_WAVES = [int(w) for w in os.environ.get("EC_WAVES", "1").split(",")]
+EC_CUS = [int(c) for c in os.environ.get("EC_CUS", "16,24,32,40").split(",")]
+cases = [(False, 1024, 0, "stride", w) for w in EC_WAVES] + [(True, 1024, 0, "stride", w) for w in EC_WAVES]
+cases += [(True, 4096, k, "first", w) for k in EC_CUS for w in EC_WAVES]
+for w in EC_WAVES:
+    eng.set_tuning("ec_waves", w)
+    rec = bench.measure_recovery(eng, torch, D=len(R["c1"]), M=len(on), T=20)
+    print(f"ec_waves={w} seed recovery alone: {rec['gpu_ms']:.3f} ms correct={rec['correct']}", flush=True)
+for overlap, mi, ec_cus, pick, w in cases:
+    eng.set_tuning("ec_waves", w)
     rec = ServerReconstruction(eng, pass1_min_items=mi, ec_cus=ec_cus, cu_pick=pick)
     with torch.cuda.stream(main):
         for _ in range(2):
@@ -43,5 +52,5 @@ for overlap, mi, ec_cus, pick in cases:
         e1.record(main)
     torch.cuda.synchronize()
     rec.close()
-    print(f"overlap={overlap} min_items={mi} ec_cus={ec_cus} pick={pick} ms={e0.elapsed_time(e1) / 5:.3f} correct={bool(torch.all(out == len(on)).item())}",
+    print(f"ec_waves={w} overlap={overlap} min_items={mi} ec_cus={ec_cus} pick={pick} ms={e0.elapsed_time(e1) / 5:.3f} correct={bool(torch.all(out == len(on)).item())}",
           flush=True)
