@@ -43,9 +43,14 @@ def client_bounds(N: int, world: int, rank: int):
 
 
 class ShardedRound:
-    """Runs one rank's share of a round on its GPU and reduce-scatters the partials."""
+    """Runs one rank's share of a round on its GPU and reduce-scatters the partials.
 
-    def __init__(self, engine, L: int, group=None, device=None):
+    With buffers=2, launch() leaves the reduce-scatter in flight (async_op) and the
+    next round's kernel writes the other partial buffer, so round k's collective over
+    xGMI runs under round k+1's kernel; a buffer is reused only after the collective
+    that read it has completed (a stream-side wait, the host never blocks)."""
+
+    def __init__(self, engine, L: int, group=None, device=None, buffers: int = 1):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -54,8 +59,13 @@ class ShardedRound:
         self.Lp = padded_length(L, self.world)
         self.lo, self.hi = shard_bounds(L, self.world, self.rank)
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.partial = torch.zeros(self.Lp, dtype=torch.int32, device=dev)
-        self.out = torch.empty(self.Lp // self.world, dtype=torch.int32, device=dev)
+        if buffers not in (1, 2):
+            raise ValueError("buffers must be 1 or 2")
+        self._partials = [torch.zeros(self.Lp, dtype=torch.int32, device=dev) for _ in range(buffers)]
+        self._outs = [torch.empty(self.Lp // self.world, dtype=torch.int32, device=dev) for _ in range(buffers)]
+        self._pending = [None] * buffers
+        self._k = 0
+        self.partial, self.out = self._partials[0], self._outs[0]
 
     def prepare_seeds(self, d_seeds, d_signs, stream=None):
         self.K = d_seeds.shape[0]
@@ -83,3 +93,41 @@ class ShardedRound:
         self.prepare_seeds(d_seeds, d_signs, stream)
         self.compute(d_rows, stream)
         return self.exchange()
+
+    def _async_ok(self):
+        # RCCL (or gloo on host tensors) can leave the collective in flight; the gloo path
+        # over a shared GPU (tests only) goes through host copies and stays synchronous
+        return self.world > 1 and not (self.partial.is_cuda and dist.get_backend(self.group) == "gloo")
+
+    def launch(self, d_rows, d_seeds, d_signs, stream=None) -> int:
+        """Enqueue one round; returns its buffer index for result()."""
+        b = self._k % len(self._partials)
+        if self._pending[b] is not None:
+            # the collective that last read this buffer: Work.wait() makes the CURRENT
+            # stream wait, so make that the stream the kernel is enqueued on
+            if stream is not None and isinstance(stream, torch.cuda.Stream):
+                with torch.cuda.stream(stream):
+                    self._pending[b].wait()
+            else:
+                self._pending[b].wait()
+            self._pending[b] = None
+        self.partial, self.out = self._partials[b], self._outs[b]
+        self.prepare_seeds(d_seeds, d_signs, stream)
+        self.compute(d_rows, stream)
+        if self._async_ok():
+            self._pending[b] = dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM,
+                                                          group=self.group, async_op=True)
+        else:
+            self.exchange()
+        self._k += 1
+        return b
+
+    def result(self, b: int | None = None):
+        """This rank's shard of round `b` (default: the last launched), after its collective."""
+        b = (self._k - 1) % len(self._partials) if b is None else b
+        if self._pending[b] is not None:
+            self._pending[b].wait()
+            self._pending[b] = None
+        if self.world == 1:
+            return self._partials[b][: self.L]
+        return self._outs[b][: self.hi - self.lo]

@@ -58,7 +58,15 @@ def worker(rank, world, port, N, K, L, q):
         c0, c1 = client_bounds(N, world, rank)
         rnd = OracleRound(None, L, device=torch.device("cpu"))
         out = rnd.step(rows[c0:c1], seeds, signs)
-        q.put((rank, rnd.lo, rnd.hi, out.numpy().view(np.uint32).copy()))
+        # pipelined: two rounds in flight on alternating buffers (async reduce-scatter),
+        # the second with its rows negated-and-reused so the two results differ
+        pipe = OracleRound(None, L, device=torch.device("cpu"), buffers=2)
+        b0 = pipe.launch(rows[c0:c1], seeds, signs)
+        b1 = pipe.launch((0 - rows[c0:c1]).astype(np.uint32), seeds, signs)
+        b2 = pipe.launch(rows[c0:c1], seeds, signs)          # reuses buffer 0 after its collective
+        r1, r2 = pipe.result(b1).numpy().view(np.uint32).copy(), pipe.result(b2).numpy().view(np.uint32).copy()
+        assert b0 == b2 == 0 and b1 == 1
+        q.put((rank, rnd.lo, rnd.hi, out.numpy().view(np.uint32).copy(), r1, r2))
     finally:
         dist.destroy_process_group()
 
@@ -77,9 +85,12 @@ def test_sharded_round_matches_single_process(world, N, K, L):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    want_neg = O.aggregate_unmask((0 - rows).astype(np.uint32), seeds, signs, threads=4)
     covered = np.zeros(L, bool)
-    for rank, lo, hi, out in got:
+    for rank, lo, hi, out, r1, r2 in got:
         assert np.array_equal(out, want[lo:hi]), rank
+        assert np.array_equal(r1, want_neg[lo:hi]), rank      # pipelined round on buffer 1
+        assert np.array_equal(r2, want[lo:hi]), rank          # buffer 0 reused
         covered[lo:hi] = True
     assert covered.all()
 
