@@ -33,6 +33,11 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident aggregate+unmask GB/s, N clients × L int32 per round"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 Tops/s
+# Measured ChaCha20 ceiling of the chip: a memory-free ChaCha kernel, compiler or hand-scheduled
+# asm, runs 612-645 G words/s (profiles/r01_chacha_probe.log, r01_chacha_{asm,full}_probe.log):
+# every ChaCha instruction costs ~3.9 cycles, so the 2-cycle simple-op rate behind VALU_PEAK_TOPS
+# is not reachable for this dependency graph.
+CHACHA_CEILING_GWORDS = 640.0
 CHACHA_OPS_PER_WORD = 60.4       # VALU instructions per mask word in items_kernel (.s count)
 
 
@@ -198,7 +203,11 @@ def main():
                      "bytes_per_launch": 4 * rows_rank * L + 4 * L},
         "roofline_valu": {"bound": "valu", "mask_words_per_launch": int(words), "ops_per_word": CHACHA_OPS_PER_WORD,
                           "achieved_tops": round(valu_tops, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
-                          "frac": round(valu_tops / VALU_PEAK_TOPS, 4)},
+                          "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
+                          "mask_gwords_per_s": round(words / (kms * 1e-3) / 1e9, 1),
+                          "measured_chacha_ceiling_gwords": CHACHA_CEILING_GWORDS,
+                          "frac_of_measured_ceiling": round(words / (kms * 1e-3) / 1e9 / CHACHA_CEILING_GWORDS, 4),
+                          "ceiling_source": "profiles/r01_chacha_probe.log, r01_chacha_asm_probe.log"},
     }
 
     tr = committed_traffic(rows_rank, L, int(K))
