@@ -64,8 +64,11 @@ struct Item {
 static_assert(sizeof(Item) == 64, "Item must be 64 bytes");
 
 // Launchers (flm_kernels.hip).  All enqueue on `stream` and return hipError_t.
+// d_zero (optional): zero-fill zero_n u32 words of the round's output in the same launch.
 hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
-                                uint32_t *d_meta, hipStream_t stream);
+                                uint32_t *d_meta, hipStream_t stream, uint32_t *d_zero = nullptr,
+                                uint64_t zero_n = 0);
+int seed_schedule_groups(int K, uint64_t zero_n);
 // items_kernel variants (see flm_kernels.hip): row load layout / accumulator form.
 enum ItemsVariant : int {
     kVarCoalesced = 0,  // coalesced rows, separate row/mask accumulators (any plan)

@@ -43,10 +43,20 @@ namespace flm {
 // One thread per seed builds its SeedRec from the raw 32 seed bytes and sign.
 // Workgroup p writes its count of negative / invalid signs to meta[2+2p],
 // meta[3+2p] and meta[0] = number of workgroups, so no zeroing pass is needed.
+// zero_out/zero_n: when the round's plan adds into its output with atomics, the same
+// launch zero-fills it (grid-stride, 16-B stores) -- one submission fewer than a memset.
 __global__ __launch_bounds__(256) void seed_schedule_kernel(const uint8_t *__restrict__ seeds,
                                                             const int8_t *__restrict__ signs, int K,
                                                             SeedRec *__restrict__ recs,
-                                                            uint32_t *__restrict__ meta) {
+                                                            uint32_t *__restrict__ meta,
+                                                            uint32_t *__restrict__ zero_out, uint64_t zero_n) {
+    if (zero_out) {
+        const uint64_t quads = zero_n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads; q += stride)
+            reinterpret_cast<uint4 *>(zero_out)[q] = make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t t = 4 * quads + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (t < zero_n) zero_out[t] = 0u;
+    }
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t neg = 0, bad = 0;
     if (k < K) {
@@ -442,10 +452,19 @@ __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t
 #undef FLM_ROTL
 
 // ----------------------------------------------------------------- launchers
+// Workgroups of the seed-schedule launch: one per 256 seeds, more when it also zero-fills
+// (about 16 KiB per workgroup, at most 1024).  meta needs 2 + 2 * this many words.
+int seed_schedule_groups(int K, uint64_t zero_n) {
+    const uint64_t g = (uint64_t)((K + 255) / 256 > 0 ? (K + 255) / 256 : 1);
+    const uint64_t z = std::min<uint64_t>(1024, (zero_n + 4095) / 4096);
+    return (int)std::max(g, z);
+}
+
 hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, int K, SeedRec *d_recs,
-                                uint32_t *d_meta, hipStream_t stream) {
-    const unsigned grid = (unsigned)((K + 255) / 256 > 0 ? (K + 255) / 256 : 1);
-    hipLaunchKernelGGL(seed_schedule_kernel, dim3(grid), dim3(256), 0, stream, d_seeds, d_signs, K, d_recs, d_meta);
+                                uint32_t *d_meta, hipStream_t stream, uint32_t *d_zero, uint64_t zero_n) {
+    const unsigned grid = (unsigned)seed_schedule_groups(K, d_zero ? zero_n : 0);
+    hipLaunchKernelGGL(seed_schedule_kernel, dim3(grid), dim3(256), 0, stream, d_seeds, d_signs, K, d_recs, d_meta,
+                       d_zero, d_zero ? zero_n : 0);
     return hipGetLastError();
 }
 

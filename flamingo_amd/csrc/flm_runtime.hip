@@ -261,7 +261,9 @@ int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     int v = ctx->tune_variant;
     // measured (tools/ab_items.py, profiles/r01_ab_items*.log): merged accumulator
     // fastest where legal (seeds spread over the rows when seed-light), block next
-    if (v < 0) v = plan.single_tile ? (plan.seed_light ? flm::kVarMergedSpread : flm::kVarMerged) : flm::kVarBlock;
+    if (v < 0)
+        v = plan.single_tile ? (plan.seed_light ? flm::kVarMergedSpread : flm::kVarMerged)
+                             : (plan.seed_light ? flm::kVarBlockSpread : flm::kVarBlock);
     if (!plan.single_tile && v >= flm::kVarMerged) v = (v == flm::kVarMergedSpread || v == flm::kVarBlockSpread)
                                                           ? flm::kVarBlockSpread : flm::kVarBlock;
     return v;
@@ -341,17 +343,22 @@ int check_range(flm_ctx *ctx, uint64_t slot_hi) {
     return 0;
 }
 
-int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s) {
+// zero_out (optional): the round's output, zero-filled by the same launch (zero_n words)
+int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s,
+                      uint32_t *zero_out = nullptr, uint64_t zero_n = 0) {
     FLM_HIP(ctx, ctx->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec)));
-    FLM_HIP(ctx, ctx->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)((std::max(K, 1) + 255) / 256))));
-    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s));
+    const int groups = flm::seed_schedule_groups(K, zero_out ? zero_n : 0);
+    FLM_HIP(ctx, ctx->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)groups)));
+    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s,
+                                           zero_out, zero_n));
     ctx->table_k = K;
     return 0;
 }
 
+// zeroed: the output was already zero-filled on this stream (by the seed-schedule launch)
 int run_plan(flm_ctx *ctx, const Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
-             size_t out_elems, hipStream_t s) {
-    if (plan.needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
+             size_t out_elems, hipStream_t s, bool zeroed = false) {
+    if (plan.needs_zero && !zeroed) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
     const int variant_id = pick_variant(ctx, plan);
     FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
                                    ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
@@ -669,8 +676,15 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (L == 0) return 0;
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
-    if (int rc = flm_seed_table_dev(ctx, d_seeds, d_signs, K, stream)) return rc;
-    return flm_aggregate_dev(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out, stream);
+    if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    int rc = 0;
+    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
+    if (!plan) return rc;
+    // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
+    if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, plan->needs_zero ? d_out : nullptr, L))) return rc;
+    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s, plan->needs_zero);
 }
 
 // A whole device-resident round captured once as a HIP graph: seed schedule,
@@ -722,13 +736,15 @@ int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitc
                           items, g->plan, ctx->tune_min_items);
     if (int rc = upload_plan(ctx, g->plan, items)) return bail(rc);
     hipError_t e = g->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec));
-    if (e == hipSuccess) e = g->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)((std::max(K, 1) + 255) / 256)));
+    if (e == hipSuccess)
+        e = g->meta.reserve(sizeof(uint32_t) *
+                            (2 + 2 * (size_t)flm::seed_schedule_groups(K, g->plan.needs_zero ? L : 0)));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
     capturing = e == hipSuccess;
     if (e == hipSuccess)
-        e = flm::launch_seed_schedule(d_seeds, d_signs, K, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), cs);
-    if (e == hipSuccess && g->plan.needs_zero) e = hipMemsetAsync(d_out, 0, L * sizeof(uint32_t), cs);
+        e = flm::launch_seed_schedule(d_seeds, d_signs, K, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), cs,
+                                      g->plan.needs_zero ? d_out : nullptr, L);
     if (e == hipSuccess)
         e = flm::launch_items(g->plan.subtiles, pick_variant(ctx, g->plan), g->plan.items.as<Item>(), g->plan.n_items,
                               d_rows, row_pitch, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), d_out, cs);
