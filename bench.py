@@ -480,16 +480,16 @@ def variant_pairs_only(eng, torch, rows, m, nbrs, online, L, stream, P):
     res = {}
     for name, rr in (("pairs_only", rows),):
         eng.seed_table_dev(d_seeds, d_signs, stream=stream)
-        for _ in range(3):
+        for _ in range(10):
             eng.aggregate_dev(rr, K, out, L=L, stream=stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
         reps = 20
-        for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        ev[0].record(stream)
+        for i in range(reps):
             eng.aggregate_dev(rr, K, out, L=L, stream=stream)
-        e1.record(stream)
+            ev[i + 1].record(stream)
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
+        ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))   # per launch, median
         gbs = (4.0 * rr.shape[0] * L + 4.0 * L) / (ms * 1e-3) / 1e9
         res[name] = {"rows": int(rr.shape[0]), "seeds_K": int(K), "kernel_ms": round(ms, 4), "GB/s": round(gbs, 1),
                      "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
