@@ -123,19 +123,6 @@ __device__ __forceinline__ Fe fe_sub(const Fe &a, const Fe &b) {
     return r;
 }
 
-// acc += a*b with the carry out of the 64-bit accumulator counted in hi: v_mad_u64_u32's own
-// carry-out feeds one v_addc, both in ONE asm statement.  Split across two statements the
-// compiler pads every boundary with s_nop (it cannot see through inline asm); together they
-// issue back to back.  tools/ec_probe.hip: 543 ns per single-wave multiply, against 669 ns
-// with the pads and 860 ns for a plain 64-bit C CIOS; bit-identical on 65536 inputs.
-__device__ __forceinline__ void mad_acc(uint64_t &acc, uint32_t &hi, uint32_t a, uint32_t b) {
-    uint64_t c;
-    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-        "v_addc_co_u32_e64 %1, %2, 0, %1, %2"
-        : "+v"(acc), "+v"(hi), "=&s"(c)
-        : "v"(a), "v"(b));
-}
-
 // Montgomery reduction of a 512-bit product t by p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in one
 // signed column pass: the quotient digit m_i is the running limb i itself (-p^-1 = 1 mod
 // 2^32) and adding m_i*p touches limbs i (-m, clears it), i+3 (+m), i+6 (+m), i+7 (-m), i+8 (+m).
@@ -160,50 +147,121 @@ __device__ __forceinline__ Fe mont_reduce(uint32_t (&t)[16]) {
     return r;
 }
 
+// A whole product column in ONE asm statement: NP mad/addc pairs, acc (64-bit) += a[q]*b[q]
+// with every carry-out of the 64-bit accumulator counted in hi (v_mad_u64_u32's own carry-out
+// feeds one v_addc).  The compiler pads each inline-asm boundary with s_nop (it cannot see
+// through asm): one statement per product pair measured 543 ns per single-wave multiply,
+// against 669 ns with mad and addc in separate statements and 860 ns for a plain 64-bit C CIOS
+// (tools/ec_probe.hip); one statement per column drops most of the remaining pads.
+#define FLM_MC(n) "v_mad_u64_u32 %[acc], %[c], %[a" #n "], %[b" #n "], %[acc]\n\t" \
+                  "v_addc_co_u32_e64 %[hi], %[c], 0, %[hi], %[c]\n\t"
+#define FLM_MI(n) [a##n] "v"(a[n]), [b##n] "v"(b[n])
+#define FLM_MO(n) , FLM_MI(n)
+// acc/hi are early-clobber: later products read inputs after the first mad/addc wrote them,
+// so no input may share their registers (the compiler otherwise reuses one holding the same
+// value, e.g. a zero limb of the constant 1 against hi's initial 0)
+#define FLM_MOUT [acc] "+&v"(acc), [hi] "+&v"(hi), [c] "=&s"(c)
+template <int NP>
+__device__ __forceinline__ void mad_col(uint64_t &acc, uint32_t &hi, const uint32_t (&a)[NP], const uint32_t (&b)[NP]) {
+    uint64_t c;
+    if constexpr (NP == 1) asm(FLM_MC(0) : FLM_MOUT : FLM_MI(0));
+    else if constexpr (NP == 2) asm(FLM_MC(0) FLM_MC(1) : FLM_MOUT : FLM_MI(0) FLM_MO(1));
+    else if constexpr (NP == 3) asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2));
+    else if constexpr (NP == 4)
+        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3));
+    else if constexpr (NP == 5)
+        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4)
+            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4));
+    else if constexpr (NP == 6)
+        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5)
+            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5));
+    else if constexpr (NP == 7)
+        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5) FLM_MC(6)
+            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5) FLM_MO(6));
+    else
+        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5) FLM_MC(6) FLM_MC(7)
+            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5) FLM_MO(6) FLM_MO(7));
+}
+#undef FLM_MC
+#undef FLM_MO
+#undef FLM_MI
+#undef FLM_MOUT
+
+// column K of a*b (products a_i b_{K-i}) into acc/hi
+template <int K>
+__device__ __forceinline__ void mul_col(uint64_t &acc, uint32_t &hi, const Fe &a, const Fe &b) {
+    constexpr int lo = K < 8 ? 0 : K - 7, top = K < 8 ? K : 7, n = top - lo + 1;
+    uint32_t av[n], bv[n];
+#pragma unroll
+    for (int q = 0; q < n; ++q) {
+        av[q] = a.v[lo + q];
+        bv[q] = b.v[K - lo - q];
+    }
+    mad_col<n>(acc, hi, av, bv);
+}
+
+// column K of the doubled cross products of a^2 (a_i a_j, i < j, i + j = K)
+template <int K>
+__device__ __forceinline__ void sqr_col(uint64_t &x, uint32_t &xh, const Fe &a) {
+    constexpr int lo = K < 8 ? 0 : K - 7, top = K >= 1 ? (K - 1) / 2 : -1, n = top - lo + 1;
+    if constexpr (n > 0) {
+        uint32_t av[n], bv[n];
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            av[q] = a.v[lo + q];
+            bv[q] = a.v[K - lo - q];
+        }
+        mad_col<n>(x, xh, av, bv);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void mul_cols(uint64_t &acc, uint32_t &hi, uint32_t (&t)[16], const Fe &a, const Fe &b) {
+    if constexpr (K < 15) {
+        mul_col<K>(acc, hi, a, b);
+        t[K] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)hi << 32);
+        hi = 0;
+        mul_cols<K + 1>(acc, hi, t, a, b);
+    }
+}
+
 // Montgomery product a*b*R^-1 mod p: product scanning with a 96-bit column accumulator
 __device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
     uint32_t t[16];
     uint64_t acc = 0;
     uint32_t hi = 0;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int j = k - i;
-            if (j < 0 || j > 7) continue;
-            mad_acc(acc, hi, a.v[i], b.v[j]);
-        }
-        t[k] = (uint32_t)acc;
-        acc = (acc >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
-    }
+    mul_cols<0>(acc, hi, t, a, b);
     t[15] = (uint32_t)acc;
     return mont_reduce(t);
+}
+
+template <int K>
+__device__ __forceinline__ void sqr_cols(uint64_t &c, uint32_t (&t)[16], const Fe &a) {
+    if constexpr (K < 15) {
+        uint64_t x = 0;
+        uint32_t xh = 0;
+        sqr_col<K>(x, xh, a);
+        xh = (xh << 1) | (uint32_t)(x >> 63);
+        x <<= 1;
+        uint64_t n = x + c;
+        xh += (n < x);
+        x = n;
+        if constexpr ((K & 1) == 0) {
+            const uint32_t av[1] = {a.v[K / 2]};
+            mad_col<1>(x, xh, av, av);
+        }
+        t[K] = (uint32_t)x;
+        c = (x >> 32) | ((uint64_t)xh << 32);
+        sqr_cols<K + 1>(c, t, a);
+    }
 }
 
 // a^2 R^-1: 28 cross products summed once and doubled, plus 8 squares (36 mads instead of 64)
 __device__ __forceinline__ Fe fe_sqr(const Fe &a) {
     uint32_t t[16];
     uint64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-        uint64_t x = 0;
-        uint32_t xh = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int j = k - i;
-            if (j <= i || j > 7) continue;
-            mad_acc(x, xh, a.v[i], a.v[j]);
-        }
-        xh = (xh << 1) | (uint32_t)(x >> 63);
-        x <<= 1;
-        uint64_t n = x + c;
-        xh += (n < x);
-        x = n;
-        if ((k & 1) == 0) mad_acc(x, xh, a.v[k / 2], a.v[k / 2]);
-        t[k] = (uint32_t)x;
-        c = (x >> 32) | ((uint64_t)xh << 32);
-    }
+    sqr_cols<0>(c, t, a);
     t[15] = (uint32_t)c;
     return mont_reduce(t);
 }
