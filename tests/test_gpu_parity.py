@@ -355,3 +355,33 @@ def test_round_graph_matches_oracle(eng, N, K, L):
         assert torch.equal(eager[:L], out[:L])
     finally:
         g.close()
+
+
+def test_device_fuzz_vs_oracle(eng):
+    """Random device-resident rounds (rows pitch, mask window, PRG slot offset, empty sets) against
+    the oracle: out[l] = sum_i rows[i][l] + [lo <= l < hi] sum_k sign_k PRG(seed_k)[prg_slot0 + l]."""
+    import torch
+    g = rng(2024)
+    for case in range(24):
+        N, K, L = int(g.integers(0, 80)), int(g.integers(0, 400)), int(g.integers(1, 40000))
+        pitch = (L + 3) // 4 * 4 + 4 * int(g.integers(0, 4))
+        lo = int(g.integers(0, L // 16 + 1)) * 16 if g.random() < 0.5 else 0
+        hi = L if g.random() < 0.5 else int(g.integers(lo, L + 1))
+        slot0 = 16 * int(g.integers(0, 1 << 16)) if g.random() < 0.5 else 0
+        rows, seeds, signs = rand_case(case, N, K, L)
+        want = O.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8), L=L, threads=8) \
+            if N else np.zeros(L, np.uint32)
+        if K and hi > lo:
+            want[lo:hi] += O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds, signs, L=hi - lo,
+                                              slot0=slot0 + lo, threads=8)
+        d_rows = torch.zeros((max(N, 1), pitch), dtype=torch.int32, device="cuda")[:N]
+        if N:
+            d_rows[:, :L] = torch.from_numpy(rows.view(np.int32)).cuda()
+        d_seeds = torch.from_numpy(seeds).cuda() if K else torch.zeros((0, 32), dtype=torch.uint8, device="cuda")
+        d_signs = torch.from_numpy(signs).cuda() if K else torch.zeros(0, dtype=torch.int8, device="cuda")
+        out = torch.full((pitch,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi, prg_slot0=slot0)
+        torch.cuda.synchronize()
+        got = out[:L].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), (case, N, K, L, pitch, lo, hi, slot0, np.flatnonzero(got != want)[:5])
+        assert np.all(out[L:].cpu().numpy() == 0x5A5A5A5A), (case, "wrote past L")
