@@ -3,7 +3,6 @@ alone (no EC beside it): does a CU mask by itself cost more than the lost CUs?""
 import os
 import sys
 
-import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -4,7 +4,6 @@ is exactly the multi-GPU code.  Checks every round's shard against the synchrono
 import os
 import sys
 
-import numpy as np
 import torch
 import torch.distributed as dist
 
