@@ -385,3 +385,32 @@ def test_device_fuzz_vs_oracle(eng):
         got = out[:L].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, want), (case, N, K, L, pitch, lo, hi, slot0, np.flatnonzero(got != want)[:5])
         assert np.all(out[L:].cpu().numpy() == 0x5A5A5A5A), (case, "wrote past L")
+
+
+def test_client_mask_dev_fuzz_vs_oracle(eng):
+    """Random device client-masking batches (SA_ClientAgent.py:304-324): ragged CSR seed lists
+    (clients with no seeds included), odd L, padded pitch, with and without explicit inputs x."""
+    import torch
+    g = rng(77)
+    for case in range(12):
+        N, L = int(g.integers(1, 40)), int(g.integers(1, 9000))
+        pitch = (L + 3) // 4 * 4 + 4 * int(g.integers(0, 3))
+        deg = g.integers(0, 9, size=N) * (g.random(N) < 0.85)
+        seg = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+        K = int(seg[-1])
+        seeds = g.integers(0, 256, size=(max(K, 1), 32), dtype=np.uint8)[:K]
+        signs = np.where(g.random(K) < 0.5, 1, -1).astype(np.int8)
+        use_x = bool(g.random() < 0.5)
+        x = g.integers(0, 2**32, size=(N, L), dtype=np.uint32) if use_x else None
+        want = O.client_mask(seg, seeds, signs, L, x=x)
+        d_seeds = torch.from_numpy(seeds.copy()).cuda() if K else torch.zeros((1, 32), dtype=torch.uint8,
+                                                                               device="cuda")
+        out = torch.full((N, pitch), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+        d_x = None
+        if use_x:
+            d_x = torch.zeros((N, pitch), dtype=torch.int32, device="cuda")
+            d_x[:, :L] = torch.from_numpy(x.view(np.int32)).cuda()
+        eng.client_mask_dev(seg, d_seeds, signs, out, L, x=d_x)
+        torch.cuda.synchronize()
+        got = out[:, :L].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want), (case, N, L, pitch, K, use_x)
