@@ -195,7 +195,7 @@ def main():
                 "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
         "config": {"workload": "c4: aggregate + self-mask and dropout-pair unmask, one server round",
                    "clients": N, "clients_per_gpu": Ng, "online": int(len(online)), "L": L, "seeds_K": int(K),
-                   "dropout_pairs_D": int(D), "global_batch": N, "seq_len": L,
+                   "dropout_pairs_D": int(D),
                    "parallelism": f"client-shard{G}+slot-shard{G}" + ("+rccl-reduce-scatter-overlapped" if G > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
