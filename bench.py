@@ -241,7 +241,8 @@ def main():
     return 0 if ok else 1
 
 
-RECON_EC_CUS = 24        # CUs given to the EC combine in the CU-split schedule (tools/recon_probe.py sweep)
+RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-split schedule (recon_probe sweep:
+                          # 24 of MI355X's 256); a multiple of the 8 XCDs so every XCD loses the same count
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
 
 
@@ -265,7 +266,9 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         from flamingo_amd.reconstruct import ServerReconstruction
         from flamingo_amd.synthetic import recovery_round
         recon, point_cache = ServerReconstruction(eng, dev), {}
-        recon_cu = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=RECON_EC_CUS,
+        ec_cus = max(1, int(round(RECON_EC_FRAC * eng.cu_count() / 8)) * 8) if eng.cu_count() >= 64 else \
+            max(1, int(round(RECON_EC_FRAC * eng.cu_count())))
+        recon_cu = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=ec_cus,
                                         cu_pick="first")
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
@@ -355,7 +358,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
             "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
                         "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
-                        f"{RECON_EC_CUS} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS})"}
+                        f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS})"}
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
