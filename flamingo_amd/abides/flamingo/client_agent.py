@@ -75,6 +75,7 @@ class SA_ClientAgent(Agent):
         self.pair_keys = {}          # neighbour -> SHA-256(a_i A_j)[:32]   (:256-263), cached across iterations
         self.committee_keys = {}     # member -> AES key (a_i A_c).x mod 2^128 (:234-236)
         self.symmetric_keys = {}     # (committee members) client -> AES key (:86-91)
+        param.register_client(self)
         if id in self.user_committee:
             ids = list(range(num_clients))
             self.symmetric_keys = self._aes_keys(ids)
@@ -127,17 +128,12 @@ class SA_ClientAgent(Agent):
             self.recordTime(t0, "REPORT")
 
     # --------------------------------------------------------------- round
-    def _ecdh(self, ids) -> np.ndarray:
-        """a_i * A_j for the given clients, one GPU batch; (len, 64) wire rows."""
-        ids = list(ids)
-        pki = param.pki(self.num_clients)
-        out, _ = param.engine().ec_mul_wire(pki.pk_wire(ids), C.scalars_to_wire([self.secret_key] * len(ids)))
-        return out
-
     def _aes_keys(self, ids) -> dict:
-        w = self._ecdh(ids)
-        return {j: (int.from_bytes(bytes(w[k, :32]), "big") & _MASK128).to_bytes(16, "big")
-                for k, j in enumerate(ids)}
+        """(a_i A_j).x mod 2^128 per client j (:234-236, :86-91); the ECDH points of every
+        client x committee pair come from one GPU batch (protocol.prefetch_committee_ecdh)."""
+        param.prefetch_committee_ecdh(self.num_clients)
+        return {j: (int.from_bytes(param.ecdh_wire(self.num_clients, self.id, j)[:32], "big") & _MASK128)
+                .to_bytes(16, "big") for j in ids}
 
     def _rand_scalar(self) -> int:
         return int.from_bytes(bytes(self.random_state.randint(0, 256, size=32, dtype=np.uint8)), "big") % P256_N
@@ -152,12 +148,14 @@ class SA_ClientAgent(Agent):
         if self.id in self.neighbors_list:
             raise RuntimeError("id itself appears in its neighbor list")
         committee = sorted(self.user_committee)
-        # ECDH keys (cached: keys do not change between iterations)
+        # ECDH keys (cached: keys do not change between iterations); the whole iteration's graph
+        # is one GPU batch (protocol.prefetch_graph_ecdh)
         missing = [j for j in nb if j not in self.pair_keys]
         if missing:
-            w = self._ecdh(missing)
-            for k, j in enumerate(missing):
-                self.pair_keys[j] = hashlib.sha256(bytes(w[k])).digest()[: self.key_length]
+            param.prefetch_graph_ecdh(self.current_iteration, self.num_clients, self.neighborhood_size)
+            for j in missing:
+                w = param.ecdh_wire(self.num_clients, self.id, j)
+                self.pair_keys[j] = hashlib.sha256(w).digest()[: self.key_length]
         if not self.committee_keys:
             self.committee_keys = self._aes_keys(committee)
 
@@ -182,13 +180,12 @@ class SA_ClientAgent(Agent):
             seeds.append(hashlib.sha256(C.point_bytes(H[j])).digest()[: self.key_length])
             signs.append(1 if self.id < j else -1)
 
-        # ElGamal under the system key: c0 = rG, c1 = H + r pk (:434-447), one GPU batch
-        rs = [self._rand_scalar() for _ in nb]
-        base = np.concatenate([np.tile(np.frombuffer(C.point_bytes(C.G), np.uint8), (len(nb), 1)),
-                               np.tile(np.frombuffer(C.point_bytes(self.system_pk), np.uint8), (len(nb), 1))])
-        out, _ = param.engine().ec_mul_wire(base, C.scalars_to_wire(rs + rs))
-        pts = C.points_from_wire(out)
-        cipher = {(self.id, j): (pts[k], C.add(H[j], pts[len(nb) + k])) for k, j in enumerate(nb)}
+        # ElGamal under the system key: c0 = rG, c1 = H + r pk (:434-447); the r G, r pk of every
+        # client of the iteration come from one GPU batch (protocol.elgamal_masks)
+        _, rg, rpk = param.elgamal_masks(self, self.current_iteration, nb)
+        c0 = C.points_from_wire(rg) if nb else []
+        rp = C.points_from_wire(rpk) if nb else []
+        cipher = {(self.id, j): (c0[k], C.add(H[j], rp[k])) for k, j in enumerate(nb)}
 
         x = None if self.input_vector is None else np.asarray(self.input_vector, np.uint32)[None, :]
         vec = param.engine().client_mask(np.array([0, len(seeds)], np.int64), seeds, signs, self.vector_len, x=x)[0]

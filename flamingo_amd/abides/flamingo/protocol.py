@@ -5,6 +5,14 @@ GPU engine of this process, and caches the committee and the per-iteration
 neighbour graph (the reference re-derives the graph in every findNeighbors
 call, util/param.py:56-103; here it is derived once per iteration for all
 clients, with the keystream computed on the GPU).
+
+The simulation's P-256 work is batched across clients, because one scalar
+multiplication is a ~3 ms latency chain on the GPU whatever the batch size
+(DESIGN.md section 5): every ECDH point a_i A_j of the iteration's graph and
+of the client x committee pairs (symmetric, so one per unordered pair), and
+every client's ElGamal r G, r pk of the iteration, are computed in one launch
+each and handed to the agents.  The values are those each client would
+compute alone (SA_ClientAgent.py:234-236, 256-263, 434-447).
 """
 from __future__ import annotations
 
@@ -24,6 +32,10 @@ _graphs: dict = {}
 _committees: dict = {}
 _pkis: dict = {}
 _h2c: dict = {}
+_ecdh: dict = {}          # (root, N, min(i,j), max(i,j)) -> 64-byte wire of a_i A_j
+_ecdh_done: set = set()   # batches already computed (graph iterations, committee)
+_clients: dict = {}       # id -> client agent (for the batched ElGamal draws)
+_elgamal: dict = {}       # (root, iteration, id) -> (r list, (deg, 64) rG wire, (deg, 64) r pk wire)
 
 
 def configure(root: bytes | None = None, L: int | None = None, committee: int | None = None):
@@ -40,6 +52,10 @@ def configure(root: bytes | None = None, L: int | None = None, committee: int | 
     _graphs.clear()
     _committees.clear()
     _pkis.clear()
+    _ecdh.clear()
+    _ecdh_done.clear()
+    _clients.clear()
+    _elgamal.clear()
 
 
 def engine():
@@ -94,3 +110,85 @@ def hash_to_curve(h_ijt: str):
         from ...crypto import hash_str_to_curve
         pt = _h2c[h_ijt] = hash_str_to_curve(h_ijt)
     return pt
+
+
+# ------------------------------------------------------- batched P-256 work
+def _ecdh_batch(num_clients: int, pairs) -> None:
+    """a_i A_j for every (i, j) in pairs not cached yet, in one GPU launch.  i == j is kept: a
+    committee member that is also a client encrypts its own m_i share under a_i A_i (:234-236)."""
+    from ... import crypto as C
+    import numpy as np
+    kp = pki(num_clients)
+    todo = sorted({(min(i, j), max(i, j)) for i, j in pairs} -
+                  {k[2:] for k in _ecdh if k[:2] == (root_seed, num_clients)})
+    if not todo:
+        return
+    a = [kp.client_sk[i] for i, _ in todo]
+    out, _ = engine().ec_mul_wire(kp.pk_wire([j for _, j in todo]), C.scalars_to_wire(a))
+    for (i, j), row in zip(todo, np.asarray(out)):
+        _ecdh[(root_seed, num_clients, i, j)] = bytes(row)
+
+
+def prefetch_graph_ecdh(iteration: int, num_clients: int, neighborhood_size: int) -> None:
+    key = ("graph", root_seed, iteration, num_clients, neighborhood_size)
+    if key in _ecdh_done:
+        return
+    nb = neighbors(iteration, num_clients, neighborhood_size)
+    _ecdh_batch(num_clients, [(i, j) for i in range(num_clients) for j in nb[i]])
+    _ecdh_done.add(key)
+
+
+def prefetch_committee_ecdh(num_clients: int) -> None:
+    key = ("committee", root_seed, num_clients, committee_size)
+    if key in _ecdh_done:
+        return
+    comm = sorted(committee(num_clients))
+    _ecdh_batch(num_clients, [(i, c) for i in range(num_clients) for c in comm])
+    _ecdh_done.add(key)
+
+
+def ecdh_wire(num_clients: int, i: int, j: int) -> bytes:
+    """a_i A_j (= a_j A_i) as 64 wire bytes x||y; computed in a batch if not prefetched."""
+    k = (root_seed, num_clients, min(i, j), max(i, j))
+    if k not in _ecdh:
+        _ecdh_batch(num_clients, [(i, j)])
+    return _ecdh[k]
+
+
+def register_client(agent) -> None:
+    _clients[agent.id] = agent
+
+
+def elgamal_masks(agent, iteration: int, nb: list):
+    """(r list, r G wire rows, r pk_system wire rows) for this client's neighbours in `iteration`
+    (SA_ClientAgent.py:434-447).  The first client to ask in an iteration draws every registered,
+    online client's r's from that client's own random state and computes all of them in one launch."""
+    from ... import crypto as C
+    import numpy as np
+    key = (root_seed, iteration, agent.id)
+    if key not in _elgamal:
+        batch = []
+        for cid in sorted(_clients):
+            c = _clients[cid]
+            if iteration in c.offline_iterations or (root_seed, iteration, cid) in _elgamal:
+                continue
+            cnb = sorted(neighbors(iteration, c.num_clients, c.neighborhood_size)[cid])
+            batch.append((cid, [c._rand_scalar() for _ in cnb]))
+        if agent.id not in [b[0] for b in batch]:
+            batch.append((agent.id, [agent._rand_scalar() for _ in nb]))
+        rs = [r for _, r_list in batch for r in r_list]
+        if rs:
+            sys_pk = pki(agent.num_clients).system_pk
+            base = np.concatenate([np.tile(np.frombuffer(C.point_bytes(C.G), np.uint8), (len(rs), 1)),
+                                   np.tile(np.frombuffer(C.point_bytes(sys_pk), np.uint8), (len(rs), 1))])
+            out, _ = engine().ec_mul_wire(base, C.scalars_to_wire(rs + rs))
+            out = np.asarray(out)
+        o = 0
+        for cid, r_list in batch:
+            n = len(r_list)
+            _elgamal[(root_seed, iteration, cid)] = (r_list, out[o:o + n] if n else None,
+                                                     out[len(rs) + o:len(rs) + o + n] if n else None)
+            o += n
+        for k in [k for k in _elgamal if k[1] < iteration - 1]:
+            del _elgamal[k]
+    return _elgamal.pop(key)
