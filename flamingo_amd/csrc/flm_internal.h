@@ -86,6 +86,13 @@ enum ItemsVariant : int {
 hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_items, const uint32_t *d_rows,
                         uint64_t row_pitch, const SeedRec *d_recs, const uint32_t *d_meta,
                         uint32_t *d_out, hipStream_t stream);
+// One-launch round for small rounds (flm_kernels.hip small_round_kernel): a workgroup owns
+// 16*B slots (B = 1, 2, 4), sums every row there and adds every seed's mask; meta gets the
+// sign counts (one part).  mask_lo % 16 == 0 and (mask_hi % 16 == 0 or mask_hi == L).
+int small_round_slots(int B);
+hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
+                              const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
+                              uint32_t ctr0, uint32_t *d_out, uint32_t *d_meta, hipStream_t stream);
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
                                const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
 

@@ -414,6 +414,169 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
     }
 }
 
+// ------------------------------------------------------- small-round kernel
+// The whole round in ONE launch for rounds too small to fill the chip through items_kernel
+// (BASELINE c2: N=128 rows, K=128 seeds, L=16384).  There, items_kernel's 1024-thread
+// workgroups land on half the CUs, and the seed-schedule launch before it adds its own gap
+// (13 us per round measured; ~3 us of ChaCha work).  Here a 256-thread workgroup owns
+// T = 16*B output slots outright.  It sums every row over them and adds every seed's mask,
+// then stores the tile once: no atomics, no zero-fill, no seed table.
+//   lane (b, sl) of wave w: ChaCha block b of the tile for seed s = pass*4*(64/B) + w*(64/B) + sl,
+//   keys read straight from the raw 32-byte seeds (no SeedRec precompute: its saving is ~5 %
+//   of a block and would cost the extra launch).
+//   Rows: thread (quad q, group rg) sums rows rg, rg + RG, ... of quad q with 16-B loads,
+//   issued before the ChaCha work so HBM latency hides under it.
+//   Combine: lane accumulators and row partials through LDS, 16 entries per thread, then
+//   one store per slot.
+// Block 0 also writes the sign counts to meta (meta[0] = 1 part) as seed_schedule_kernel does,
+// so flm_check_signs keeps working.
+template <int B>
+__global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__restrict__ rows, uint64_t pitch, int N,
+                                                          const uint8_t *__restrict__ seeds,
+                                                          const int8_t *__restrict__ signs, int K, uint64_t L,
+                                                          uint64_t mask_lo, uint64_t mask_hi, uint32_t ctr0,
+                                                          uint32_t *__restrict__ out, uint32_t *__restrict__ meta) {
+    constexpr int T = 16 * B;     // slots per workgroup
+    constexpr int SPW = 64 / B;   // seeds per wave per pass
+    constexpr int SPP = 4 * SPW;  // seeds per pass
+    constexpr int Q = T / 4;      // 16-B quads per row tile
+    constexpr int RG = 256 / Q;   // row groups
+    constexpr int G = 256 / T;    // slot groups of the combine
+    constexpr int RB = 4;         // rows per thread in flight under the ChaCha work
+    __shared__ __attribute__((aligned(16))) uint32_t lm[256 * 16];  // lane accumulators, 16 KiB
+    __shared__ __attribute__((aligned(16))) uint32_t lr[RG * T];    // row partials
+    __shared__ uint32_t lp[G * T];                                  // per-group slot partials (256 words)
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t slot0 = (uint64_t)blockIdx.x * T;
+
+    // ---- rows: the first RB of this thread's rows are loaded before the masks
+    const int q = tid % Q, rg = tid / Q;
+    const uint64_t qslot = slot0 + 4 * (uint64_t)q;
+    const bool qok = qslot < L;  // a quad straddling L stays inside the row (pitch >= round_up(L, 4))
+    const uint32_t *rq = rows + qslot;
+    u32x4 racc = u32x4(0u), rv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+        const int r = rg + u * RG;
+        rv[u] = (qok && r < N) ? *reinterpret_cast<const u32x4 *>(rq + (uint64_t)r * pitch) : u32x4(0u);
+    }
+
+    // ---- masks: one ChaCha block per lane per pass
+    uint32_t acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0;
+    uint32_t nneg = 0;
+    const int b = lane % B, sl = lane / B;
+    const uint64_t bslot = slot0 + 16 * (uint64_t)b;
+    if (bslot >= mask_lo && bslot < mask_hi) {
+        const uint32_t ctr = ctr0 + (uint32_t)(bslot / 16);
+        const bool al16 = ((uintptr_t)seeds & 15) == 0;
+        for (int s = w * SPW + sl; s < K; s += SPP) {
+            const uint8_t *p = seeds + 32 * (size_t)s;
+            uint32_t k[8];
+            if (al16) {
+                const uint4 a0 = reinterpret_cast<const uint4 *>(p)[0], a1 = reinterpret_cast<const uint4 *>(p)[1];
+                k[0] = a0.x; k[1] = a0.y; k[2] = a0.z; k[3] = a0.w;
+                k[4] = a1.x; k[5] = a1.y; k[6] = a1.z; k[7] = a1.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    k[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
+                           ((uint32_t)p[4 * i + 3] << 24);
+            }
+            const bool neg = signs[s] < 0;
+            const uint32_t xc = neg ? ~kAbcd : kAbcd;  // -(ks ^ C) = (ks ^ ~C) + 1
+            nneg += neg ? 1u : 0u;
+            uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
+            uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+            uint32_t x12 = ctr, x13 = 0u, x14 = 0u, x15 = 0u;
+#pragma unroll
+            for (int r = 0; r < 10; ++r) {
+                FLM_QR(x0, x4, x8, x12);
+                FLM_QR(x1, x5, x9, x13);
+                FLM_QR(x2, x6, x10, x14);
+                FLM_QR(x3, x7, x11, x15);
+                FLM_QR(x0, x5, x10, x15);
+                FLM_QR(x1, x6, x11, x12);
+                FLM_QR(x2, x7, x8, x13);
+                FLM_QR(x3, x4, x9, x14);
+            }
+            acc[0] += (x0 + kSigma0) ^ xc;
+            acc[1] += (x1 + kSigma1) ^ xc;
+            acc[2] += (x2 + kSigma2) ^ xc;
+            acc[3] += (x3 + kSigma3) ^ xc;
+            acc[4] += (x4 + k[0]) ^ xc;
+            acc[5] += (x5 + k[1]) ^ xc;
+            acc[6] += (x6 + k[2]) ^ xc;
+            acc[7] += (x7 + k[3]) ^ xc;
+            acc[8] += (x8 + k[4]) ^ xc;
+            acc[9] += (x9 + k[5]) ^ xc;
+            acc[10] += (x10 + k[6]) ^ xc;
+            acc[11] += (x11 + k[7]) ^ xc;
+            acc[12] += (x12 + ctr) ^ xc;
+            acc[13] += x13 ^ xc;
+            acc[14] += x14 ^ xc;
+            acc[15] += x15 ^ xc;
+        }
+    }
+
+    // ---- rows: add the first batch, stream the rest
+#pragma unroll
+    for (int u = 0; u < RB; ++u) racc = racc + rv[u];
+    if (qok)
+        for (int r = rg + RB * RG; r < N; r += RG) racc = racc + *reinterpret_cast<const u32x4 *>(rq + (uint64_t)r * pitch);
+
+    // ---- combine
+    u32x4 *lm4 = reinterpret_cast<u32x4 *>(lm) + 4 * tid;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        lm4[j] = u32x4{acc[4 * j] + nneg, acc[4 * j + 1] + nneg, acc[4 * j + 2] + nneg, acc[4 * j + 3] + nneg};
+    *reinterpret_cast<u32x4 *>(lr + rg * T + 4 * q) = racc;
+    __syncthreads();
+    {
+        const int j = tid % T, g = tid / T;
+        const int jb = j / 16, jw = j % 16;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int e = g * 16; e < g * 16 + 16; ++e) {  // 16 of the 256/B (wave, seed-lane) entries of slot j
+            const int wv = e / SPW, sle = e % SPW;
+            sum += lm[(wv * 64 + sle * B + jb) * 16 + jw];
+        }
+#pragma unroll
+        for (int r = g; r < RG; r += G) sum += lr[r * T + j];
+        lp[g * T + j] = sum;
+    }
+    __syncthreads();
+    if (tid < T) {
+        uint32_t total = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) total += lp[g * T + tid];
+        if (slot0 + tid < L) out[slot0 + tid] = total;
+    }
+
+    // ---- sign counts (block 0), the same meta layout as seed_schedule_kernel with one part
+    if (blockIdx.x == 0) {
+        uint32_t n = 0, bad = 0;
+        for (int s = tid; s < K; s += 256) {
+            const int sg = signs[s];
+            n += sg < 0 ? 1u : 0u;
+            bad += (sg != 1 && sg != -1) ? 1u : 0u;
+        }
+        __syncthreads();  // lp is free again
+        lp[tid] = n;
+        lm[tid] = bad;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tn = 0, tb = 0;
+            for (int i = 0; i < 256; ++i) { tn += lp[i]; tb += lm[i]; }
+            meta[0] = 1u;
+            meta[2] = tn;
+            meta[3] = tb;
+        }
+    }
+}
+
 // --------------------------------------------------- byte keystream (host PRF)
 // out = in ^ ChaCha20(key, nonce) from block `counter`, one block per thread.
 __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t k1, uint32_t k2,
@@ -502,6 +665,25 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
     }
 #undef FLM_V
 #undef FLM_L
+    return hipGetLastError();
+}
+
+int small_round_slots(int B) { return 16 * B; }
+
+hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
+                              const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
+                              uint32_t ctr0, uint32_t *d_out, uint32_t *d_meta, hipStream_t stream) {
+    const uint64_t T = (uint64_t)small_round_slots(B);
+    const unsigned grid = (unsigned)((L + T - 1) / T);
+    switch (B) {
+        case 1: hipLaunchKernelGGL(small_round_kernel<1>, dim3(grid), dim3(256), 0, stream, d_rows, pitch, N, d_seeds,
+                                   d_signs, K, L, mask_lo, mask_hi, ctr0, d_out, d_meta); break;
+        case 2: hipLaunchKernelGGL(small_round_kernel<2>, dim3(grid), dim3(256), 0, stream, d_rows, pitch, N, d_seeds,
+                                   d_signs, K, L, mask_lo, mask_hi, ctr0, d_out, d_meta); break;
+        case 4: hipLaunchKernelGGL(small_round_kernel<4>, dim3(grid), dim3(256), 0, stream, d_rows, pitch, N, d_seeds,
+                                   d_signs, K, L, mask_lo, mask_hi, ctr0, d_out, d_meta); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

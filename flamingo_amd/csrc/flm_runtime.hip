@@ -77,6 +77,9 @@ using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t
 
 }  // namespace
 
+// flm_last_plan's variant for a round run by small_round_kernel (items = its workgroups)
+constexpr int kSmallRoundVariant = 100;
+
 struct flm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -101,6 +104,7 @@ struct flm_ctx {
     int tune_min_items = 1024;  // planner target for work items per aggregate launch
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
+    int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
 };
 
@@ -340,6 +344,28 @@ int check_range(flm_ctx *ctx, uint64_t slot_hi) {
     if (slot_hi > (1ull << 36))
         return fail(ctx, FLM_ERANGE, "PRG slot range ends at %llu > 2^36 (block counter high word must stay 0)",
                     (unsigned long long)slot_hi);
+    return 0;
+}
+
+// Workgroup width B (16*B slots) of the one-launch small-round kernel for this round, or 0 to
+// take the seed-schedule + items_kernel path.  Auto (tune_small 1): rounds whose rows and mask
+// words are both <= 2^22 (c2: 2^21 each), where items_kernel's fixed ~10 us dominates.
+int small_round_width(const flm_ctx *ctx, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi) {
+    if (ctx->tune_small == 0) return 0;
+    if (mask_lo % 16 || (mask_hi % 16 && mask_hi != L)) return 0;
+    if (ctx->tune_small == 1 && ((uint64_t)N * L > (1ull << 22) || (uint64_t)K * (mask_hi - mask_lo) > (1ull << 22)))
+        return 0;
+    // 2 blocks per 256-thread workgroup keeps 128 seeds per pass (c2: one pass, every lane busy);
+    // longer vectors take 4 (64 slots) so the grid stays near 1024 workgroups
+    return L >= (1ull << 16) ? 4 : 2;
+}
+
+int run_small_round(flm_ctx *ctx, int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
+                    const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi, uint64_t prg_slot0,
+                    uint32_t *d_out, DevBuf &meta, hipStream_t s) {
+    FLM_HIP(ctx, meta.reserve(4 * sizeof(uint32_t)));
+    FLM_HIP(ctx, flm::launch_small_round(B, d_rows, pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi,
+                                         (uint32_t)(prg_slot0 / 16), d_out, meta.as<uint32_t>(), s));
     return 0;
 }
 
@@ -680,6 +706,18 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     int rc = 0;
+    if (const int B = small_round_width(ctx, N, K, L, mask_lo, mask_hi)) {
+        // one submission; the device seed table is not built, so flm_aggregate_dev must not reuse it
+        if ((rc = run_small_round(ctx, B, d_rows, row_pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi, prg_slot0,
+                                  d_out, ctx->meta, s)))
+            return rc;
+        ctx->table_k = -1;
+        ctx->last_items = (int)((L + flm::small_round_slots(B) - 1) / flm::small_round_slots(B));
+        ctx->last_tile = flm::small_round_slots(B);
+        ctx->last_atomics = 0;
+        ctx->last_variant = kSmallRoundVariant;
+        return 0;
+    }
     Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
     if (!plan) return rc;
     // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
@@ -731,10 +769,13 @@ int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitc
         delete g;
         return code;
     };
+    const int B = small_round_width(ctx, N, K, L, mask_lo, mask_hi);
     std::vector<Item> items;
-    build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0,
-                          items, g->plan, ctx->tune_min_items);
-    if (int rc = upload_plan(ctx, g->plan, items)) return bail(rc);
+    if (!B) {
+        build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0,
+                              items, g->plan, ctx->tune_min_items);
+        if (int rc = upload_plan(ctx, g->plan, items)) return bail(rc);
+    }
     hipError_t e = g->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec));
     if (e == hipSuccess)
         e = g->meta.reserve(sizeof(uint32_t) *
@@ -742,10 +783,13 @@ int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitc
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
     capturing = e == hipSuccess;
-    if (e == hipSuccess)
+    if (e == hipSuccess && B)
+        e = flm::launch_small_round(B, d_rows, row_pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi,
+                                    (uint32_t)(prg_slot0 / 16), d_out, g->meta.as<uint32_t>(), cs);
+    if (e == hipSuccess && !B)
         e = flm::launch_seed_schedule(d_seeds, d_signs, K, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), cs,
                                       g->plan.needs_zero ? d_out : nullptr, L);
-    if (e == hipSuccess)
+    if (e == hipSuccess && !B)
         e = flm::launch_items(g->plan.subtiles, pick_variant(ctx, g->plan), g->plan.items.as<Item>(), g->plan.n_items,
                               d_rows, row_pitch, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), d_out, cs);
     if (e == hipSuccess) {
@@ -949,6 +993,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "ec_waves") {
         if (value != 1 && value != 4 && value != 8) return fail(ctx, FLM_EINVAL, "ec_waves must be 1, 4 or 8");
         ctx->tune_ec_waves = value;
+    } else if (k == "small") {
+        if (value < 0 || value > 2) return fail(ctx, FLM_EINVAL, "small must be 0 (never), 1 (auto) or 2 (when legal)");
+        ctx->tune_small = value;
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;

@@ -135,7 +135,8 @@ int flm_check_signs(flm_ctx *ctx, int *bad_count);
 /* ----------------------------------------------------------- diagnostics */
 
 /* Describe the launch plan the last *aggregate* call used:
- * items, tile slots, atomics used (0/1), kernel variant id. */
+ * items, tile slots, atomics used (0/1), kernel variant id (100: the one-launch
+ * small-round kernel, items = its workgroups). */
 int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics, int *variant);
 
 /* Tuning knobs for A/B measurement (defaults are the tuned choice):
@@ -151,7 +152,12 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "ec_threads" 64 (default) | 128 | 256 lanes per workgroup of the P-256
  *              scalar-multiplication kernel.
  *   "ec_waves" 1 (default: uncapped registers) | 4 | 8 minimum waves per SIMD the
- *              scalar-multiplication kernel is compiled for (more waves, more spills). */
+ *              scalar-multiplication kernel is compiled for (more waves, more spills).
+ *   "small"    0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
+ *              rounds as ONE small-round launch never | when rows and mask words are both
+ *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or
+ *              mask_hi == L).  That path builds no device seed table: a following
+ *              flm_aggregate_dev needs its own flm_seed_table_dev. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the

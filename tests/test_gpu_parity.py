@@ -414,3 +414,82 @@ def test_client_mask_dev_fuzz_vs_oracle(eng):
         torch.cuda.synchronize()
         got = out[:, :L].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, want), (case, N, L, pitch, K, use_x)
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_small_round_path_vs_oracle(eng, mode):
+    """The one-launch small-round kernel (flm_set_tuning "small" 2: whenever the window allows it)
+    and the seed-schedule + items path ("small" 0) against the oracle on the same random rounds:
+    K past one 128/64-seed pass, N past the 128 rows a thread batches, L odd and past 2^16
+    (64-slot tiles), windows, PRG slot offsets, unaligned seed rows, empty sets; and the sign
+    counts flm_check_signs reads back."""
+    import torch
+    g = rng(4242 + mode)
+    eng.set_tuning("small", mode)
+    try:
+        for case in range(14):
+            N, K = int(g.integers(0, 300)), int(g.integers(0, 600))
+            L = int(g.integers(1, 20000)) if case % 3 else int(g.integers(1 << 16, 90000))
+            pitch = (L + 3) // 4 * 4 + 4 * int(g.integers(0, 3))
+            lo = int(g.integers(0, L // 16 + 1)) * 16 if g.random() < 0.5 else 0
+            hi = L if g.random() < 0.5 else int(g.integers(lo // 16, L // 16 + 1)) * 16
+            hi = max(hi, lo)
+            slot0 = 16 * int(g.integers(0, 1 << 20)) if g.random() < 0.5 else 0
+            rows, seeds, signs = rand_case(9000 + case, N, K, L)
+            want = O.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8), L=L, threads=8) \
+                if N else np.zeros(L, np.uint32)
+            if K and hi > lo:
+                want[lo:hi] += O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds, signs, L=hi - lo,
+                                                  slot0=slot0 + lo, threads=8)
+            d_rows = torch.zeros((max(N, 1), pitch), dtype=torch.int32, device="cuda")[:N]
+            if N:
+                d_rows[:, :L] = torch.from_numpy(rows.view(np.int32)).cuda()
+            if K and case % 2:  # seed rows at an odd byte offset: the byte-load key path
+                buf = torch.zeros(K * 32 + 1, dtype=torch.uint8, device="cuda")
+                buf[1:] = torch.from_numpy(seeds.reshape(-1)).cuda()
+                d_seeds = buf[1:].view(K, 32)
+            else:
+                d_seeds = torch.from_numpy(seeds).cuda() if K else torch.zeros((0, 32), dtype=torch.uint8,
+                                                                               device="cuda")
+            d_signs = torch.from_numpy(signs).cuda() if K else torch.zeros(0, dtype=torch.int8, device="cuda")
+            out = torch.full((pitch,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, mask_lo=lo, mask_hi=hi, prg_slot0=slot0)
+            torch.cuda.synchronize()
+            small = eng.last_plan()["variant"] == 100
+            assert small == (mode == 2), (case, eng.last_plan())
+            got = out[:L].cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want), (case, mode, N, K, L, pitch, lo, hi, slot0,
+                                               np.flatnonzero(got != want)[:5])
+            assert np.all(out[L:].cpu().numpy() == 0x5A5A5A5A), (case, "wrote past L")
+            assert eng.check_signs() == 0
+        # an invalid sign is counted by either path
+        rows, seeds, signs = rand_case(1, 4, 40, 1000)
+        signs[7] = 3
+        out = torch.empty(1000, dtype=torch.int32, device="cuda")
+        eng.aggregate_unmask_dev(torch.from_numpy(rows.view(np.int32)).cuda(), torch.from_numpy(seeds).cuda(),
+                                 torch.from_numpy(signs).cuda(), out, L=1000)
+        torch.cuda.synchronize()
+        assert eng.check_signs() == 1
+    finally:
+        eng.set_tuning("small", 1)
+
+
+def test_small_round_default_routing(eng):
+    """Auto mode: c2 (N=128, L=16384) takes the one-launch kernel, c3-sized rounds do not; a
+    flm_aggregate_dev after a small round must not silently reuse a seed table it never built."""
+    import torch
+    N, K, L = 128, 128, 16384
+    rows, seeds, signs = rand_case(5, N, K, L)
+    d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+    d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L)
+    torch.cuda.synchronize()
+    assert eng.last_plan() == {"items": L // 32, "tile_slots": 32, "atomics": 0, "variant": 100}
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), O.aggregate_unmask(rows, seeds, signs, threads=8))
+    with pytest.raises(RuntimeError, match="seed table"):
+        eng.aggregate_dev(d_rows, K, out, L=L)
+    big = torch.zeros((64, 1 << 17), dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(big, d_seeds, d_signs, torch.empty(1 << 17, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    assert eng.last_plan()["variant"] != 100
