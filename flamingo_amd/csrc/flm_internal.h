@@ -93,6 +93,11 @@ int small_round_slots(int B);
 hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
                               const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
                               uint32_t ctr0, uint32_t *d_out, uint32_t *d_meta, hipStream_t stream);
+// Client masking with the same kernel (SEG mode): grid (L/256, N), row i gets seeds
+// [d_seg[i], d_seg[i+1]) on top of x row i (or the constant `bias` when d_x is NULL).
+hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, const int64_t *d_seg,
+                                   const uint8_t *d_seeds, const int8_t *d_signs, uint64_t L, uint32_t bias,
+                                   uint32_t *d_out, hipStream_t stream);
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
                                const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
 

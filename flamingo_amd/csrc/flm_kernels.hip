@@ -430,12 +430,17 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
 //   one store per slot.
 // Block 0 also writes the sign counts to meta (meta[0] = 1 part) as seed_schedule_kernel does,
 // so flm_check_signs keeps working.
-template <int B>
+// SEG (client masking, SA_ClientAgent.py:304-324): blockIdx.y is output row i; its seeds are
+// [seg[i], seg[i+1]), its input is row i of `rows` (none: the all-ones input, `bias` = 1), and
+// the row is written at out + i*pitch.  No sign counts (the host validated the signs).
+template <int B, bool SEG = false>
 __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__restrict__ rows, uint64_t pitch, int N,
                                                           const uint8_t *__restrict__ seeds,
                                                           const int8_t *__restrict__ signs, int K, uint64_t L,
                                                           uint64_t mask_lo, uint64_t mask_hi, uint32_t ctr0,
-                                                          uint32_t *__restrict__ out, uint32_t *__restrict__ meta) {
+                                                          uint32_t *__restrict__ out, uint32_t *__restrict__ meta,
+                                                          const int64_t *__restrict__ seg = nullptr,
+                                                          uint32_t bias = 0u) {
     constexpr int T = 16 * B;     // slots per workgroup
     constexpr int SPW = 64 / B;   // seeds per wave per pass
     constexpr int SPP = 4 * SPW;  // seeds per pass
@@ -449,6 +454,15 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t slot0 = (uint64_t)blockIdx.x * T;
+    int k_lo = 0, k_hi = K;
+    if constexpr (SEG) {
+        const uint64_t y = blockIdx.y;
+        k_lo = (int)seg[y];
+        k_hi = (int)seg[y + 1];
+        N = rows ? 1 : 0;
+        if (rows) rows += y * pitch;
+        out += y * pitch;
+    }
 
     // ---- rows: the first RB of this thread's rows are loaded before the masks
     const int q = tid % Q, rg = tid / Q;
@@ -472,7 +486,7 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
     if (bslot >= mask_lo && bslot < mask_hi) {
         const uint32_t ctr = ctr0 + (uint32_t)(bslot / 16);
         const bool al16 = ((uintptr_t)seeds & 15) == 0;
-        for (int s = w * SPW + sl; s < K; s += SPP) {
+        for (int s = k_lo + w * SPW + sl; s < k_hi; s += SPP) {
             const uint8_t *p = seeds + 32 * (size_t)s;
             uint32_t k[8];
             if (al16) {
@@ -549,14 +563,14 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
     }
     __syncthreads();
     if (tid < T) {
-        uint32_t total = 0;
+        uint32_t total = bias;
 #pragma unroll
         for (int g = 0; g < G; ++g) total += lp[g * T + tid];
         if (slot0 + tid < L) out[slot0 + tid] = total;
     }
 
     // ---- sign counts (block 0), the same meta layout as seed_schedule_kernel with one part
-    if (blockIdx.x == 0) {
+    if (!SEG && blockIdx.x == 0) {
         uint32_t n = 0, bad = 0;
         for (int s = tid; s < K; s += 256) {
             const int sg = signs[s];
@@ -684,6 +698,16 @@ hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int
                                    d_signs, K, L, mask_lo, mask_hi, ctr0, d_out, d_meta); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, const int64_t *d_seg,
+                                   const uint8_t *d_seeds, const int8_t *d_signs, uint64_t L, uint32_t bias,
+                                   uint32_t *d_out, hipStream_t stream) {
+    constexpr int B = 16;  // 256-slot tiles: 4 seeds x 16 blocks per wave, 16 seeds per pass
+    const dim3 grid((unsigned)((L + 16 * B - 1) / (16 * B)), (unsigned)N);
+    hipLaunchKernelGGL((small_round_kernel<B, true>), grid, dim3(256), 0, stream, d_x, pitch, 0, d_seeds, d_signs, 0,
+                       L, (uint64_t)0, L, 0u, d_out, (uint32_t *)nullptr, d_seg, bias);
     return hipGetLastError();
 }
 

@@ -84,7 +84,8 @@ struct flm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out;
+    DevBuf rows, out, seeds, signs, segs, recs, meta, bytes_in, bytes_out;
+    std::vector<uint8_t> seg_host;  // packed seg + signs of the last small client-mask launch
     DevBuf ec_in, ec_base, ec_scal, ec_jac, ec_out, ec_dig, ec_flags;  // P-256 batches
     // pinned staging ring for pageable host rows: two buffers, each reused once
     // the DMA that read it has completed (event per buffer)
@@ -612,7 +613,7 @@ void flm_free(flm_ctx *ctx) {
         delete kv.second;
     }
     ctx->scratch_plan.items.release();
-    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
+    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->segs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
                       &ctx->bytes_out, &ctx->ec_in, &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out,
                       &ctx->ec_dig, &ctx->ec_flags})
         b->release();
@@ -866,6 +867,26 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     if (int rc = check_range(ctx, L)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
+    // small batches (c2: 128 clients x ~15 seeds x 16384 slots): one launch of the small-round
+    // kernel, one workgroup per (client, 256-slot tile), instead of a seed schedule + one 1024-thread
+    // workgroup per client row.  seg and signs travel in ONE host-to-device copy.
+    if (ctx->tune_small == 2 || (ctx->tune_small == 1 && (uint64_t)K * L <= (1ull << 26))) {
+        const size_t seg_bytes = (size_t)(N + 1) * sizeof(int64_t);
+        std::vector<uint8_t> &meta_h = ctx->seg_host;  // outlives the call (pageable copy source)
+        meta_h.resize(seg_bytes + (size_t)K);
+        std::memcpy(meta_h.data(), seg, seg_bytes);
+        if (K > 0) std::memcpy(meta_h.data() + seg_bytes, signs, (size_t)K);
+        FLM_HIP(ctx, ctx->segs.reserve(meta_h.size()));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->segs.p, meta_h.data(), meta_h.size(), hipMemcpyHostToDevice, s));
+        FLM_HIP(ctx, flm::launch_small_client_mask(d_x, pitch, N, ctx->segs.as<int64_t>(), d_seeds,
+                                                   reinterpret_cast<const int8_t *>(ctx->segs.as<uint8_t>() + seg_bytes),
+                                                   L, d_x ? 0u : 1u, d_out, s));
+        ctx->last_items = (int)(((L + 255) / 256) * (uint64_t)N);
+        ctx->last_tile = 256;
+        ctx->last_atomics = 0;
+        ctx->last_variant = kSmallRoundVariant;
+        return 0;
+    }
     // signs go to the device with the seeds (the schedule folds them into xorc)
     FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
     if (K > 0) FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, s));

@@ -493,3 +493,40 @@ def test_small_round_default_routing(eng):
     eng.aggregate_unmask_dev(big, d_seeds, d_signs, torch.empty(1 << 17, dtype=torch.int32, device="cuda"))
     torch.cuda.synchronize()
     assert eng.last_plan()["variant"] != 100
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_client_mask_small_vs_oracle(eng, mode):
+    """Client masking (SA_ClientAgent.py:304-324) through the one-launch small kernel (SEG mode,
+    "small" 2) and through the seed schedule + items path ("small" 0): rows with no seeds, rows
+    with more than one 16-seed pass, odd L past several 256-slot tiles, with and without x."""
+    import torch
+    g = rng(31 + mode)
+    eng.set_tuning("small", mode)
+    try:
+        for case in range(8):
+            N, L = int(g.integers(1, 24)), int(g.integers(1, 3000))
+            pitch = (L + 3) // 4 * 4 + 4 * int(g.integers(0, 3))
+            deg = g.integers(0, 40, size=N) * (g.random(N) < 0.8)
+            seg = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+            K = int(seg[-1])
+            seeds = g.integers(0, 256, size=(max(K, 1), 32), dtype=np.uint8)[:K]
+            signs = np.where(g.random(K) < 0.5, 1, -1).astype(np.int8)
+            x = g.integers(0, 2**32, size=(N, L), dtype=np.uint32) if case % 2 else None
+            want = O.client_mask(seg, seeds, signs, L, x=x)
+            d_seeds = torch.from_numpy(seeds.copy()).cuda() if K else torch.zeros((1, 32), dtype=torch.uint8,
+                                                                                   device="cuda")
+            out = torch.full((N, pitch), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+            d_x = None
+            if x is not None:
+                d_x = torch.zeros((N, pitch), dtype=torch.int32, device="cuda")
+                d_x[:, :L] = torch.from_numpy(x.view(np.int32)).cuda()
+            eng.client_mask_dev(seg, d_seeds, signs, out, L, x=d_x)
+            torch.cuda.synchronize()
+            assert (eng.last_plan()["variant"] == 100) == (mode == 2), (case, eng.last_plan())
+            got = out[:, :L].cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, want), (case, mode, N, L, pitch, K)
+            if pitch > L:
+                assert np.all(out[:, L:].cpu().numpy() == 0x3C3C3C3C), (case, "wrote past L")
+    finally:
+        eng.set_tuning("small", 1)
