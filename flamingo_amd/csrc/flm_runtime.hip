@@ -870,7 +870,7 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     // small batches (c2: 128 clients x ~15 seeds x 16384 slots): one launch of the small-round
     // kernel, one workgroup per (client, 256-slot tile), instead of a seed schedule + one 1024-thread
     // workgroup per client row.  seg and signs travel in ONE host-to-device copy.
-    if (ctx->tune_small == 2 || (ctx->tune_small == 1 && (uint64_t)K * L <= (1ull << 26))) {
+    if (N <= 65535 /* grid.y */ && (ctx->tune_small == 2 || (ctx->tune_small == 1 && (uint64_t)K * L <= (1ull << 26)))) {
         const size_t seg_bytes = (size_t)(N + 1) * sizeof(int64_t);
         std::vector<uint8_t> &meta_h = ctx->seg_host;  // outlives the call (pageable copy source)
         meta_h.resize(seg_bytes + (size_t)K);
