@@ -167,7 +167,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kms = float(np.mean([a.elapsed_time(b) for a, b in kern_ms]))
+    kern_list = [a.elapsed_time(b) for a, b in kern_ms]
+    kms = float(np.mean(kern_list))
+    kq = np.percentile(kern_list, [10, 50, 90])
 
     # ---- correctness of the timed round: out == |U| in every slot of my shard
     out = rnd.result()
@@ -200,6 +202,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "items_kernel<1>", "kernel_ms": round(kms, 4),
+                     "kernel_ms_p10_p50_p90": [round(float(x), 4) for x in kq],
                      "bytes_per_launch": 4 * rows_rank * L + 4 * L},
         "roofline_valu": {"bound": "valu", "mask_words_per_launch": int(words), "ops_per_word": CHACHA_OPS_PER_WORD,
                           "achieved_tops": round(valu_tops, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
