@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profile session for the committed profiles/: bench (live numbers), kernel trace + stats of
 # the same command, then separate PMC passes (no trace domains combined with --pmc).
-# usage: tools_gpu_prof.sh TAG   (outputs under gpurun_out/prof_TAG*)
+# usage: tools/gpu_prof.sh TAG   (outputs under gpurun_out/prof_TAG*)
 TAG=${1:-r01}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
