@@ -10,7 +10,8 @@ masked vectors of L = 2^20 uint32 slots; the round has N_total = 1024 * G
 clients, no dropouts, so K = N_total self-mask seeds are regenerated
 (SA_ServiceAgent.py:529-536) and the output is sum(y_i) - sum PRG(m_i) = |U|
 in every slot (checked after timing).  Per-GPU work is fixed as G grows
-(weak scaling): rows 1024 x L per GPU, masks K x L/G per GPU.
+(weak scaling): rows 1024 x L per GPU, masks K x L/G per GPU.  --total-clients N runs
+BASELINE c4 literally instead (strong scaling: N clients in all, N/G rows per GPU).
 
 A step = one round on device-resident inputs: seed-schedule launch +
 row-sum/unmask launch (+ RCCL reduce-scatter of the L-slot partial for G > 1).
@@ -47,6 +48,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clients-per-gpu", type=int, default=1024)
+    ap.add_argument("--total-clients", type=int, default=0,
+                    help="strong scaling: this many clients in all, split over the ranks (BASELINE c4 literally: "
+                         "1024 over 8 GPUs); default 0 = weak scaling, --clients-per-gpu on every rank")
     ap.add_argument("--log2-L", type=int, default=20)
     ap.add_argument("--dropout", type=float, default=0.0, help="fraction of clients offline (c5: 0.01)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -88,8 +92,9 @@ def main():
 
     eng = MaskEngine(torch.cuda.current_device())
     L = 1 << args.log2_L
-    Ng = args.clients_per_gpu
-    N = Ng * G
+    strong = args.total_clients > 0
+    N = args.total_clients if strong else args.clients_per_gpu * G
+    Ng = N // G if strong else args.clients_per_gpu
     cfg = f"c4-n{N}-L{L}"
 
     # ---- inputs: valid masked rows, built on this GPU by the client-side kernel
@@ -191,7 +196,8 @@ def main():
 
     res = {
         "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": G, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u32", "correct": ok,
         "data": "synthetic: valid masked rows y_i = 1 + PRG(m_i) +- PRG(s_ij) made on-GPU from SHA-256 bench "
                 "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
