@@ -111,8 +111,7 @@ def main():
     seg = np.array(seg_l, np.int64)
     cseeds = np.frombuffer(b"".join(seeds_l), np.uint8).reshape(-1, 32)
     csigns = np.array(signs_l, np.int8)
-    rows = torch.empty((c1 - c0, L), dtype=torch.int32, device=dev)
-    eng.client_mask_dev(seg, torch.from_numpy(cseeds.copy()).to(dev), csigns, rows, L)
+    d_cseeds = torch.from_numpy(cseeds.copy()).to(dev)
 
     g = np.random.Generator(np.random.PCG64(12345))
     n_off = int(round(args.dropout * N))
@@ -122,16 +121,22 @@ def main():
     K = sseeds.shape[0]
     D = K - len(online)
     my_online = online[(online >= c0) & (online < c1)] - c0
-    rows_on = rows if len(my_online) == rows.shape[0] else rows[torch.from_numpy(my_online).to(dev)].contiguous()
     d_seeds = torch.from_numpy(sseeds).to(dev)
     d_signs = torch.from_numpy(ssigns).to(dev)
-    torch.cuda.synchronize()
 
     # all round work (both launches and the reduce-scatter) on one dedicated stream
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     # two partial buffers: round k's reduce-scatter (RCCL, async) runs under round k+1's kernel
     rnd = ShardedRound(eng, L, buffers=2 if G > 1 else 1)
+
+    # the rows are built last, right before the warm-up: the host-side preparation above leaves
+    # the GPU idle, and MI355X ramps its clock back up over ~30 ms of load
+    # (profiles/r01_c4_launch_series.log), so the warm-up starts on a busy GPU
+    rows = torch.empty((c1 - c0, L), dtype=torch.int32, device=dev)
+    eng.client_mask_dev(seg, d_cseeds, csigns, rows, L, stream=stream)
+    rows_on = rows if len(my_online) == rows.shape[0] else rows[torch.from_numpy(my_online).to(dev)].contiguous()
+    torch.cuda.synchronize()
 
     class _Timed:
         """ShardedRound.compute bracketed by HIP events on the round's stream."""
