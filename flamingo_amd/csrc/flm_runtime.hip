@@ -861,7 +861,12 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     if (!seg || !d_out) return fail(ctx, FLM_EINVAL, "NULL argument");
     if (pitch % 4 || pitch < round_up(L, 4)) return fail(ctx, FLM_EINVAL, "pitch must be a multiple of 4 and >= L");
     if (((uintptr_t)d_out & 15) || ((uintptr_t)d_x & 15)) return fail(ctx, FLM_EINVAL, "x/out must be 16-byte aligned");
+    // seg sizes the launch: a decreasing pair would wrap a seed count and read past the table
+    if (seg[0] != 0) return fail(ctx, FLM_EINVAL, "seg[0] must be 0");
+    for (int i = 0; i < N; ++i)
+        if (seg[i + 1] < seg[i]) return fail(ctx, FLM_EINVAL, "seg must be non-decreasing");
     const int64_t K = seg[N];
+    if (K > 0x7fffffff) return fail(ctx, FLM_EINVAL, "too many seeds");
     if (K > 0 && (!d_seeds || !signs)) return fail(ctx, FLM_EINVAL, "NULL seeds/signs");
     if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;

@@ -166,6 +166,18 @@ def test_bad_arguments_raise(eng):
         eng.aggregate_unmask([rows[0], rows[1][:10]], seeds, signs)
     with pytest.raises(RuntimeError):
         eng.mask_accumulate(seeds, signs, np.zeros(32, np.uint32), slot0=8)
+    # device client masking: seg sizes the launch, so a decreasing or offset seg is refused
+    import torch
+    d_seeds = torch.from_numpy(seeds).cuda()
+    out = torch.empty((2, 64), dtype=torch.int32, device="cuda")
+    for mode in (0, 2):
+        eng.set_tuning("small", mode)
+        try:
+            for bad in ([0, 2, 1], [1, 1, 2]):
+                with pytest.raises(RuntimeError, match="seg"):
+                    eng.client_mask_dev(np.array(bad, np.int64), d_seeds, signs, out, 64)
+        finally:
+            eng.set_tuning("small", 1)
 
 
 # -------------------------------------------------------- device-resident
