@@ -85,7 +85,11 @@ struct flm_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     DevBuf rows, out, seeds, signs, segs, recs, meta, bytes_in, bytes_out;
-    std::vector<uint8_t> seg_host;  // packed seg + signs of the last small client-mask launch
+    // pinned staging for the packed seg + signs of a small client-mask launch; reused once the
+    // copy that read it has completed (event)
+    void *seg_pin = nullptr;
+    size_t seg_pin_cap = 0;
+    hipEvent_t seg_pin_done = nullptr;
     DevBuf ec_in, ec_base, ec_scal, ec_jac, ec_out, ec_dig, ec_flags;  // P-256 batches
     // pinned staging ring for pageable host rows: two buffers, each reused once
     // the DMA that read it has completed (event per buffer)
@@ -617,6 +621,9 @@ void flm_free(flm_ctx *ctx) {
                       &ctx->bytes_out, &ctx->ec_in, &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out,
                       &ctx->ec_dig, &ctx->ec_flags})
         b->release();
+    if (ctx->seg_pin_done) (void)hipEventSynchronize(ctx->seg_pin_done);
+    if (ctx->seg_pin) (void)hipHostFree(ctx->seg_pin);
+    if (ctx->seg_pin_done) (void)hipEventDestroy(ctx->seg_pin_done);
     for (int i = 0; i < 2; ++i) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
         if (ctx->stage_done[i]) (void)hipEventDestroy(ctx->stage_done[i]);
@@ -876,13 +883,21 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     // kernel, one workgroup per (client, 256-slot tile), instead of a seed schedule + one 1024-thread
     // workgroup per client row.  seg and signs travel in ONE host-to-device copy.
     if (N <= 65535 /* grid.y */ && (ctx->tune_small == 2 || (ctx->tune_small == 1 && (uint64_t)K * L <= (1ull << 26)))) {
-        const size_t seg_bytes = (size_t)(N + 1) * sizeof(int64_t);
-        std::vector<uint8_t> &meta_h = ctx->seg_host;  // outlives the call (pageable copy source)
-        meta_h.resize(seg_bytes + (size_t)K);
-        std::memcpy(meta_h.data(), seg, seg_bytes);
-        if (K > 0) std::memcpy(meta_h.data() + seg_bytes, signs, (size_t)K);
-        FLM_HIP(ctx, ctx->segs.reserve(meta_h.size()));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->segs.p, meta_h.data(), meta_h.size(), hipMemcpyHostToDevice, s));
+        const size_t seg_bytes = (size_t)(N + 1) * sizeof(int64_t), need = seg_bytes + (size_t)K;
+        if (ctx->seg_pin_done) FLM_HIP(ctx, hipEventSynchronize(ctx->seg_pin_done));  // last copy has read it
+        else FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->seg_pin_done, hipEventDisableTiming));
+        if (ctx->seg_pin_cap < need) {
+            if (ctx->seg_pin) FLM_HIP(ctx, hipHostFree(ctx->seg_pin));
+            ctx->seg_pin = nullptr;
+            ctx->seg_pin_cap = 0;
+            FLM_HIP(ctx, hipHostMalloc(&ctx->seg_pin, need, hipHostMallocDefault));
+            ctx->seg_pin_cap = need;
+        }
+        std::memcpy(ctx->seg_pin, seg, seg_bytes);
+        if (K > 0) std::memcpy(static_cast<uint8_t *>(ctx->seg_pin) + seg_bytes, signs, (size_t)K);
+        FLM_HIP(ctx, ctx->segs.reserve(need));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->segs.p, ctx->seg_pin, need, hipMemcpyHostToDevice, s));
+        FLM_HIP(ctx, hipEventRecord(ctx->seg_pin_done, s));
         FLM_HIP(ctx, flm::launch_small_client_mask(d_x, pitch, N, ctx->segs.as<int64_t>(), d_seeds,
                                                    reinterpret_cast<const int8_t *>(ctx->segs.as<uint8_t>() + seg_bytes),
                                                    L, d_x ? 0u : 1u, d_out, s));
