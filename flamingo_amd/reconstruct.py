@@ -24,6 +24,15 @@ the rest.  Unpartitioned, an EC wave resident on a SIMD leaves too few VGPRs for
 a second unmask workgroup on that CU, so those CUs run at half rate for the
 whole combine and finish last; partitioned, the unmask is evenly spread over
 the CUs it owns.  The pair pass then runs on the caller's stream over all CUs.
+
+`pair_split = f > 0` (with `ec_cus`): once the combine is done, the EC CUs do not idle
+until the self-mask pass ends.  They add the pair masks of slots [0, f*L) into a second
+partial row while the self-mask pass still runs on the other CUs.  The last pass then
+sums the two partial rows over all L and adds the pair masks of [f*L, L) only:
+
+  side (EC CUs):   ec_combine -> pair masks [0, fL) -> part[1] ------------\
+  part (the rest): shamir -> rows + self masks       -> part[0] -----------+-> part[0] + part[1]
+                                                                              + pair masks [fL, L) -> out
 """
 from __future__ import annotations
 
@@ -31,9 +40,21 @@ import torch
 
 
 class ServerReconstruction:
-    def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride"):
+    def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride",
+                 pair_split: float = 0.0):
         self.eng = engine
         self.pass1_min_items = pass1_min_items
+        if not 0.0 <= pair_split < 1.0:
+            raise ValueError("pair_split must be in [0, 1)")
+        if pair_split and ec_cus <= 0:
+            raise ValueError("pair_split needs CU-partitioned streams (ec_cus > 0)")
+        self.pair_split = float(pair_split)
+        # the side stream's pair pass builds a device seed table while the self-mask pass builds
+        # another on the other stream: a context of its own, so the two never share recs/meta
+        self.side_eng = None
+        if self.pair_split:
+            from .engine import MaskEngine
+            self.side_eng = MaskEngine(engine.device)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self._bufs = {}
         self._cu_streams = []
@@ -54,6 +75,10 @@ class ServerReconstruction:
         """The CU-partitioned streams belong to the engine (cached per CU set, destroyed
         by MaskEngine.close()); nothing of ours outlives the last run's events."""
         self._cu_streams = []
+        if self.side_eng is not None:
+            torch.cuda.synchronize(self.device)
+            self.side_eng.close()
+            self.side_eng = None
 
     def _buf(self, name, shape, dtype, fill=None):
         b = self._bufs.get(name)
@@ -101,7 +126,15 @@ class ServerReconstruction:
             main = self.part
         eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
         pitch = rows.shape[1]
-        tmp = self._buf("tmp", (1, pitch), torch.int32)
+        # part[0]: rows + self masks; part[1]: the side stream's share of the pair masks
+        part = self._buf("tmp", (2 if self.pair_split else 1, pitch), torch.int32)
+        tmp = part[:1]
+        lo = int(self.pair_split * L) // 1024 * 1024 if self.pair_split else 0
+        if lo:
+            self.side_eng.aggregate_unmask_dev(None, p_seeds, pair_signs, part[1], L=L, mask_lo=0, mask_hi=lo,
+                                               stream=self.side)
+            done = torch.cuda.Event()
+            done.record(self.side)
         if self.pass1_min_items != 1024:
             eng.set_tuning("min_items", self.pass1_min_items)
         try:
@@ -119,7 +152,8 @@ class ServerReconstruction:
         # touched is safe to free or reuse in the caller's stream order (no
         # record_stream, which would tie the allocator to a stream we may destroy)
         main.wait_event(done)
-        eng.aggregate_unmask_dev(tmp, p_seeds, pair_signs, out, L=L, stream=main)
+        eng.aggregate_unmask_dev(part if lo else tmp, p_seeds, pair_signs, out, L=L, mask_lo=lo, mask_hi=L,
+                                 stream=main)
         return out, flags
 
 

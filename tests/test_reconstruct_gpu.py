@@ -42,7 +42,9 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
     t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
     rec = ServerReconstruction(eng)
     split = ServerReconstruction(eng, ec_cus=24, cu_pick="first", pass1_min_items=4096)  # CU-partitioned
-    for overlap, rec in ((True, rec), (False, rec), (True, split)):
+    # CU-partitioned, and the EC CUs add the pair masks of the first 40 % of the slots
+    pair_split = ServerReconstruction(eng, ec_cus=32, cu_pick="first", pass1_min_items=4096, pair_split=0.4)
+    for overlap, rec in ((True, rec), (False, rec), (True, split), (True, pair_split)):
         out = torch.empty(L, dtype=torch.int32, device=dev)
         _, flags = rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out,
                            overlap=overlap)
@@ -53,5 +55,6 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
         # the recovered seeds are exactly the round's server seeds, in recon order
         assert np.array_equal(rec._bufs["seeds"].cpu().numpy(), R["server_seeds"])
     split.close()
+    pair_split.close()
     if n_off:
         assert R["D"] > 0
