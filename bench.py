@@ -258,6 +258,8 @@ def main():
 RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-split schedule (recon_probe sweep:
                           # 24 of MI355X's 256); a multiple of the 8 XCDs so every XCD loses the same count
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
+RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 24 / 32 / 40 CUs ->
+                                # 9.97 / 9.75 / 11.05 ms at c5; profiles/r01_recon_queue_sweep.log)
 
 
 def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False, recovery=False):
@@ -275,7 +277,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
     per_round, per_round_graph, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], [], True, [], [], [], [], []
-    rec_seq, rec_ovl, rec_cu, rec_ok = [], [], [], True
+    rec_seq, rec_ovl, rec_cu, rec_q, rec_ok = [], [], [], [], True
     if recovery:
         from flamingo_amd.reconstruct import ServerReconstruction
         from flamingo_amd.synthetic import recovery_round
@@ -284,6 +286,10 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             max(1, int(round(RECON_EC_FRAC * eng.cu_count())))
         recon_cu = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=ec_cus,
                                         cu_pick="first")
+        q_cus = max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count() / 8)) * 8) if eng.cu_count() >= 64 else \
+            max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count())))
+        recon_q = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=q_cus, cu_pick="first",
+                                       pair_queue=True)
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         n_off = int(round(dropout * N))
@@ -344,7 +350,8 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         if recovery:
             rt = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares",
                                                               "pair_signs")}
-            for rc, overlap, acc in ((recon, False, rec_seq), (recon, True, rec_ovl), (recon_cu, True, rec_cu)):
+            for rc, overlap, acc in ((recon, False, rec_seq), (recon, True, rec_ovl), (recon_cu, True, rec_cu),
+                                     (recon_q, True, rec_q)):
                 args = (r_on, L, rt["lambdas"], rt["mi_shares"], rt["c1"], rt["pair_shares"], rt["pair_signs"], out)
                 out.fill_(0)
                 rc.run(*args, stream=stream, overlap=overlap)
@@ -371,10 +378,15 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "sequential_ms": round(float(np.mean(rec_seq)), 4),
             "overlapped_ms": round(float(np.mean(rec_ovl)), 4),
             "cu_split_ms": round(float(np.mean(rec_cu)), 4),
+            "cu_split_queue_ms": round(float(np.mean(rec_q)), 4),
             "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
             "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
                         "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
-                        f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS})"}
+                        f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS}); "
+                        f"cu_split_queue: EC on {recon_q.ec_cus} CUs, which then claim pair-mask units from a "
+                        "device work queue until the self-mask pass ends; the last pass takes the rest on all CUs"}
+        recon_cu.close()
+        recon_q.close()
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),

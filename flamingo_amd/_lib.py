@@ -48,6 +48,8 @@ SIGNATURES = {
     "flm_ec_mul": (_int, [_vp, _u8p, _u8p, _int, _u8p, _u32p]),
     "flm_shamir_combine": (_int, [_vp, _u8p, _u8p, _int, _int, _u8p]),
     "flm_shamir_combine_dev": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
+    "flm_pair_units_dev": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp, _int, _int, _vp]),
+    "flm_flag_set_dev": (_int, [_vp, _vp, _vp]),
     "flm_round_graph_create": (_int, [_vp, _vp, _sz, _int, _vp, _vp, _int, _sz, _sz, _sz, _u64, _vp, _vp]),
     "flm_round_graph_launch": (_int, [_vp, _vp, _vp]),
     "flm_round_graph_destroy": (_int, [_vp, _vp]),

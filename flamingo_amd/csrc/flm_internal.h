@@ -98,6 +98,11 @@ hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int
 hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, const int64_t *d_seg,
                                    const uint8_t *d_seeds, const int8_t *d_signs, uint64_t L, uint32_t bias,
                                    uint32_t *d_out, hipStream_t stream);
+uint32_t pair_units_count(int K, uint64_t L, uint32_t *n_tiles);
+hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *d_dst, uint64_t L, uint32_t *d_ws,
+                             int groups, hipStream_t stream);
+hipError_t launch_flag_set(uint32_t *d_ws, hipStream_t stream);
+hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst, uint64_t n, hipStream_t stream);
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
                                const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
 

@@ -625,6 +625,84 @@ __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t
     for (uint64_t i = 0; i < m; ++i) out[off + i] = in[off + i] ^ (uint8_t)(ks[i >> 2] >> (8 * (i & 3)));
 }
 
+// ------------------------------------------------------- pair-mask work queue
+// The dropout-pair masks of the CU-split reconstruction (reconstruct.py, pair_queue=True;
+// SA_ServiceAgent.py:587-603) cut into units of (1024-slot tile, kUnitSeeds seeds), claimed
+// from a counter so that two launches on different CU sets share them without a fixed split:
+//   SIDE  (the EC CUs, once the combine is done): claims units until ws[1] (set on the
+//         self-mask stream by flag_set_kernel when that pass ends) reads non-zero;
+//   FINAL (all CUs, after both streams): claims the rest.
+// A claimed unit is always finished, so every unit is added exactly once whatever the timing:
+// the flag only moves the split.  No wave ever waits on the flag (it is read between units),
+// so both grids drain on their own.  One wave per workgroup: the LDS transpose needs only a
+// wave-local barrier, and waves that stop at different units never wait for each other.
+// Units are chunk-major (consecutive claims hit different tiles); each lane makes ChaCha
+// block `tile*64 + lane`, the 16 words go through LDS so that every u32 atomic add of the
+// wave covers 64 consecutive slots.
+constexpr int kUnitSeeds = 16;
+
+template <bool SIDE>
+__global__ __launch_bounds__(64) void pair_units_kernel(const SeedRec *__restrict__ recs, int K,
+                                                        uint32_t *__restrict__ dst, uint64_t L,
+                                                        uint32_t n_tiles, uint32_t n_units,
+                                                        uint32_t *__restrict__ ws) {
+    __shared__ uint32_t lds[64 * 17];
+    const int lane = threadIdx.x;
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) {
+            u = n_units;  // "stop"
+            if (!SIDE || __hip_atomic_load(&ws[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                u = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+        if (u >= n_units) break;
+        const uint32_t tile = u % n_tiles, chunk = u / n_tiles;
+        const int k0 = (int)chunk * kUnitSeeds;
+        const int k1 = min(K, k0 + kUnitSeeds);
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = 0u;
+        uint32_t nneg = 0;
+        const uint32_t ctr = tile * 64u + (uint32_t)lane;
+        for (int k = k0; k < k1; ++k) {
+            chacha_mask_add(&recs[k], ctr, m);
+            nneg += (recs[k].xorc != kAbcd);
+        }
+        __syncthreads();  // the previous unit's reads of lds are done
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lds[lane * 17 + i] = m[i] + nneg;
+        __syncthreads();
+        const uint64_t base = (uint64_t)tile * 1024u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int e = j * 64 + lane;
+            const uint64_t slot = base + (uint64_t)e;
+            if (slot < L)
+                __hip_atomic_fetch_add(&dst[slot], lds[(e >> 4) * 17 + (e & 15)], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ws[1] = 1 once every earlier launch on this stream has finished (release, device scope).
+__global__ void flag_set_kernel(uint32_t *__restrict__ ws) {
+    if (threadIdx.x == 0) __hip_atomic_store(&ws[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// dst = a + b (mod 2^32), 16-B accesses, grid-stride.
+__global__ __launch_bounds__(256) void add2_kernel(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
+                                                   uint32_t *__restrict__ dst, uint64_t n) {
+    const uint64_t quads = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t q = t0; q < quads; q += stride) {
+        const uint4 x = reinterpret_cast<const uint4 *>(a)[q], y = reinterpret_cast<const uint4 *>(b)[q];
+        reinterpret_cast<uint4 *>(dst)[q] = make_uint4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+    }
+    const uint64_t t = 4 * quads + t0;
+    if (t < n) dst[t] = a[t] + b[t];
+}
+
 #undef FLM_QR
 #undef FLM_ROTL
 
@@ -708,6 +786,39 @@ hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, 
     const dim3 grid((unsigned)((L + 16 * B - 1) / (16 * B)), (unsigned)N);
     hipLaunchKernelGGL((small_round_kernel<B, true>), grid, dim3(256), 0, stream, d_x, pitch, 0, d_seeds, d_signs, 0,
                        L, (uint64_t)0, L, 0u, d_out, (uint32_t *)nullptr, d_seg, bias);
+    return hipGetLastError();
+}
+
+uint32_t pair_units_count(int K, uint64_t L, uint32_t *n_tiles) {
+    const uint64_t t = (L + 1023) / 1024, c = (uint64_t)((K + kUnitSeeds - 1) / kUnitSeeds);
+    if (n_tiles) *n_tiles = (uint32_t)t;
+    const uint64_t n = t * c;
+    return n > 0xF0000000ull ? 0xFFFFFFFFu : (uint32_t)n;  // caller rejects the sentinel
+}
+
+hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *d_dst, uint64_t L, uint32_t *d_ws,
+                             int groups, hipStream_t stream) {
+    uint32_t n_tiles = 0;
+    const uint32_t n_units = pair_units_count(K, L, &n_tiles);
+    if (n_units == 0 || groups <= 0) return hipSuccess;
+    if (side)
+        hipLaunchKernelGGL(pair_units_kernel<true>, dim3(groups), dim3(64), 0, stream, d_recs, K, d_dst, L, n_tiles,
+                           n_units, d_ws);
+    else
+        hipLaunchKernelGGL(pair_units_kernel<false>, dim3(groups), dim3(64), 0, stream, d_recs, K, d_dst, L, n_tiles,
+                           n_units, d_ws);
+    return hipGetLastError();
+}
+
+hipError_t launch_flag_set(uint32_t *d_ws, hipStream_t stream) {
+    hipLaunchKernelGGL(flag_set_kernel, dim3(1), dim3(64), 0, stream, d_ws);
+    return hipGetLastError();
+}
+
+hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint64_t g = std::min<uint64_t>(2048, (n / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(add2_kernel, dim3((unsigned)g), dim3(256), 0, stream, d_a, d_b, d_dst, n);
     return hipGetLastError();
 }
 

@@ -1145,6 +1145,35 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
     return 0;
 }
 
+int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, const uint32_t *d_p0,
+                       const uint32_t *d_p1, uint32_t *d_dst, size_t L, uint32_t *d_ws, int final_pass, int groups,
+                       void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
+    if (groups <= 0) return fail(ctx, FLM_EINVAL, "groups must be positive");
+    if (!d_dst || !d_ws || (K > 0 && (!d_seeds || !d_signs))) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (final_pass && (!d_p0 || !d_p1)) return fail(ctx, FLM_EINVAL, "the final pass needs both partial rows");
+    if (final_pass && (((uintptr_t)d_p0 | (uintptr_t)d_p1 | (uintptr_t)d_dst) & 15))
+        return fail(ctx, FLM_EINVAL, "partial rows and dst must be 16-byte aligned");
+    if (L > ((uint64_t)1 << 36)) return fail(ctx, FLM_EINVAL, "L=%zu beyond the 2^32-block ChaCha counter", L);
+    if (flm::pair_units_count(K, L, nullptr) == 0xFFFFFFFFu) return fail(ctx, FLM_EINVAL, "too many units");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (final_pass) FLM_HIP(ctx, flm::launch_add2(d_p0, d_p1, d_dst, L, s));
+    if (L == 0 || K == 0) return 0;
+    if (int rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s)) return rc;
+    FLM_HIP(ctx, flm::launch_pair_units(!final_pass, ctx->recs.as<flm::SeedRec>(), K, d_dst, L, d_ws, groups, s));
+    return 0;
+}
+
+int flm_flag_set_dev(flm_ctx *ctx, uint32_t *d_ws, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (!d_ws) return fail(ctx, FLM_EINVAL, "NULL argument");
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_HIP(ctx, flm::launch_flag_set(d_ws, static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
 int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambdas, int T, int M,
                        uint8_t *seeds_out) {
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");

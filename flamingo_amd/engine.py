@@ -407,6 +407,23 @@ class MaskEngine:
         self._check(rc, "flm_ec_combine_dev")
         return seeds_out
 
+    def pair_units_dev(self, seeds, signs, dst, L: int, ws, groups: int, p0=None, p1=None, final: bool = False,
+                       stream=None):
+        """Pair masks as a shared work queue (flm_pair_units_dev): seeds (K,32) uint8, signs (K,) int8,
+        dst (>= L) int32, ws (>= 2) int32 CUDA tensors.  final=False adds the units claimed before
+        ws[1] is set into dst; final=True writes dst = p0 + p1 plus the units left."""
+        K = seeds.shape[0] if seeds is not None else 0
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
+        rc = self.lib.flm_pair_units_dev(self.ctx, vp(seeds), vp(signs), K, vp(p0), vp(p1), vp(dst), L, vp(ws),
+                                         1 if final else 0, int(groups), self._stream_handle(stream))
+        self._check(rc, "flm_pair_units_dev")
+        return dst
+
+    def flag_set_dev(self, ws, stream=None):
+        """ws[1] = 1 once the work enqueued before it on `stream` is done (flm_flag_set_dev)."""
+        self._check(self.lib.flm_flag_set_dev(self.ctx, ctypes.c_void_p(ws.data_ptr()), self._stream_handle(stream)),
+                    "flm_flag_set_dev")
+
     def check_signs(self) -> int:
         bad = ctypes.c_int()
         self._check(self.lib.flm_check_signs(self.ctx, ctypes.byref(bad)), "flm_check_signs")

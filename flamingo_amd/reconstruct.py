@@ -33,6 +33,17 @@ sums the two partial rows over all L and adds the pair masks of [f*L, L) only:
   side (EC CUs):   ec_combine -> pair masks [0, fL) -> part[1] ------------\
   part (the rest): shamir -> rows + self masks       -> part[0] -----------+-> part[0] + part[1]
                                                                               + pair masks [fL, L) -> out
+
+`pair_queue=True` (with `ec_cus`) makes that split dynamic.  The pair masks are cut into
+units of (1024 slots, 16 seeds) claimed from one device counter (flm_pair_units_dev).  The
+EC CUs claim units into part[1] from the end of the combine until the self-mask stream sets
+a stop flag; the last pass writes part[0] + part[1] and claims the rest on all CUs.  A static f
+has a cliff (the side pass outlasting the self-mask pass costs more than it saves); the queue
+stops at the flag whatever the box's EC and unmask times are:
+
+  side (EC CUs):   ec_combine -> claim units -> part[1] (until the flag) --\
+  part (the rest): shamir -> rows + self masks -> part[0] -> set flag -----+-> part[0] + part[1]
+                                                                              + units left -> out
 """
 from __future__ import annotations
 
@@ -41,18 +52,21 @@ import torch
 
 class ServerReconstruction:
     def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride",
-                 pair_split: float = 0.0):
+                 pair_split: float = 0.0, pair_queue: bool = False):
         self.eng = engine
         self.pass1_min_items = pass1_min_items
         if not 0.0 <= pair_split < 1.0:
             raise ValueError("pair_split must be in [0, 1)")
-        if pair_split and ec_cus <= 0:
-            raise ValueError("pair_split needs CU-partitioned streams (ec_cus > 0)")
+        if (pair_split or pair_queue) and ec_cus <= 0:
+            raise ValueError("pair_split / pair_queue need CU-partitioned streams (ec_cus > 0)")
+        if pair_split and pair_queue:
+            raise ValueError("pair_split and pair_queue are alternatives")
         self.pair_split = float(pair_split)
+        self.pair_queue = bool(pair_queue)
         # the side stream's pair pass builds a device seed table while the self-mask pass builds
         # another on the other stream: a context of its own, so the two never share recs/meta
         self.side_eng = None
-        if self.pair_split:
+        if self.pair_split or self.pair_queue:
             from .engine import MaskEngine
             self.side_eng = MaskEngine(engine.device)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -114,6 +128,9 @@ class ServerReconstruction:
             eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=main)
             eng.aggregate_unmask_dev(rows, seeds, signs, out, L=L, stream=main)
             return out, flags
+        if self.pair_queue:
+            return self._run_queue(rows, L, lambdas, mi_shares, c1, pair_shares, pair_signs, out, main,
+                                   m_seeds, p_seeds, flags)
         ready = torch.cuda.Event()
         ready.record(main)                       # inputs enqueued on main are visible to the side stream
         self.side.wait_event(ready)
@@ -154,6 +171,43 @@ class ServerReconstruction:
         main.wait_event(done)
         eng.aggregate_unmask_dev(part if lo else tmp, p_seeds, pair_signs, out, L=L, mask_lo=lo, mask_hi=L,
                                  stream=main)
+        return out, flags
+
+
+    def _run_queue(self, rows, L, lambdas, mi_shares, c1, pair_shares, pair_signs, out, caller, m_seeds, p_seeds,
+                   flags):
+        eng, side_eng = self.eng, self.side_eng
+        pitch = rows.shape[1]
+        part = self._buf("tmp", (2, pitch), torch.int32)
+        ws = self._buf("ws", (4,), torch.int32)
+        with torch.cuda.stream(caller):
+            ws.zero_()                           # unit counter, stop flag
+            part[1].zero_()                      # the side pass adds into it
+        ready = torch.cuda.Event()
+        ready.record(caller)
+        self.side.wait_event(ready)
+        self.part.wait_event(ready)
+        eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
+        side_groups = self.ec_cus * 32           # one-wave workgroups, 8 per SIMD
+        side_eng.pair_units_dev(p_seeds, pair_signs, part[1], L, ws, side_groups, stream=self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=self.part)
+        if self.pass1_min_items != 1024:
+            eng.set_tuning("min_items", self.pass1_min_items)
+        try:
+            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (m_seeds.shape[0],), torch.int8, -1), part[0],
+                                     L=L, stream=self.part)
+        finally:
+            if self.pass1_min_items != 1024:
+                eng.set_tuning("min_items", 1024)
+        eng.flag_set_dev(ws, stream=self.part)
+        fin = torch.cuda.Event()
+        fin.record(self.part)
+        caller.wait_event(fin)
+        caller.wait_event(done)
+        side_eng.pair_units_dev(p_seeds, pair_signs, out, L, ws, eng.cu_count() * 32, p0=part[0], p1=part[1],
+                                final=True, stream=caller)
         return out, flags
 
 

@@ -203,6 +203,20 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
  * big-endian integer (any value < 2^256), lambdas[j] < n the Lagrange
  * coefficients at 0.  shares: T*M*32 bytes, term-major.  The seeds are the
  * ChaCha20 keys of the self masks (sign -1), ready for flm_seed_table_dev. */
+/* Dropout-pair masks (SA_ServiceAgent.py:587-603) as a work queue shared by two launches on
+ * different CU sets, for the CU-split reconstruction (flamingo_amd/reconstruct.py).  Units of
+ * (1024 slots, 16 seeds) are claimed from d_ws[0]; every claimed unit is finished, so each unit
+ * is added exactly once.
+ *   final_pass = 0: d_dst[l] += sum sigma PRG(seed)[l] over the units claimed before d_ws[1]
+ *                   reads non-zero (d_dst and d_ws zeroed by the caller beforehand);
+ *   final_pass = 1: d_dst = d_p0 + d_p1, then the remaining units are added into d_dst.
+ * groups = one-wave workgroups of the launch.  Slot l uses PRG word l (prg_slot0 = 0). */
+int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, const uint32_t *d_p0,
+                       const uint32_t *d_p1, uint32_t *d_dst, size_t L, uint32_t *d_ws, int final_pass, int groups,
+                       void *stream);
+/* d_ws[1] = 1 once the work enqueued before it on `stream` has finished: the stop flag of a
+ * final_pass = 0 launch running on another stream. */
+int flm_flag_set_dev(flm_ctx *ctx, uint32_t *d_ws, void *stream);
 int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambdas, int T, int M,
                        uint8_t *seeds_out);
 int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t *d_lambdas, int T, int M,

@@ -44,7 +44,9 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
     split = ServerReconstruction(eng, ec_cus=24, cu_pick="first", pass1_min_items=4096)  # CU-partitioned
     # CU-partitioned, and the EC CUs add the pair masks of the first 40 % of the slots
     pair_split = ServerReconstruction(eng, ec_cus=32, cu_pick="first", pass1_min_items=4096, pair_split=0.4)
-    for overlap, rec in ((True, rec), (False, rec), (True, split), (True, pair_split)):
+    # CU-partitioned, the EC CUs claim pair-mask units from a queue until the self-mask pass ends
+    queue = ServerReconstruction(eng, ec_cus=32, pass1_min_items=4096, pair_queue=True)
+    for overlap, rec in ((True, rec), (False, rec), (True, split), (True, pair_split), (True, queue)):
         out = torch.empty(L, dtype=torch.int32, device=dev)
         _, flags = rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out,
                            overlap=overlap)
@@ -56,5 +58,57 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
         assert np.array_equal(rec._bufs["seeds"].cpu().numpy(), R["server_seeds"])
     split.close()
     pair_split.close()
+    queue.close()
     if n_off:
         assert R["D"] > 0
+
+
+@pytest.mark.parametrize("K,L", [(37, 5000), (100, 1 << 16), (1, 1024), (16, 17)])
+@pytest.mark.parametrize("stop", ["never", "at_once"])
+def test_pair_units_queue_vs_oracle(eng, K, L, stop):
+    """flm_pair_units_dev: a side pass then a final pass over the same counter add every
+    (1024-slot, 16-seed) unit exactly once, whichever pass claims it: with the stop flag never
+    set the side pass takes all units, set beforehand it takes none."""
+    import torch
+    import oracle as O
+    g = np.random.Generator(np.random.PCG64(K * 7 + L))
+    seeds = g.integers(0, 256, (K, 32), dtype=np.uint8)
+    signs = np.where(g.integers(0, 2, K) == 1, 1, -1).astype(np.int8)
+    p0 = g.integers(0, 1 << 32, L, dtype=np.uint64).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    ds, dg = torch.from_numpy(seeds).to(dev), torch.from_numpy(signs).to(dev)
+    pitch = (L + 3) // 4 * 4
+    part = torch.zeros((2, pitch), dtype=torch.int32, device=dev)
+    part[0, :L] = torch.from_numpy(p0.view(np.int32)).to(dev)
+    ws = torch.zeros(4, dtype=torch.int32, device=dev)
+    if stop == "at_once":
+        eng.flag_set_dev(ws)
+    eng.pair_units_dev(ds, dg, part[1], L, ws, groups=8)
+    out = torch.empty(pitch, dtype=torch.int32, device=dev)
+    eng.pair_units_dev(ds, dg, out, L, ws, groups=64, p0=part[0], p1=part[1], final=True)
+    torch.cuda.synchronize()
+    n_units = ((L + 1023) // 1024) * ((K + 15) // 16)
+    claimed = int(ws[0].item())
+    if stop == "never":
+        assert int(part[1, :L].ne(0).sum()) > 0
+    else:
+        assert int(part[1].abs().sum()) == 0
+    assert claimed >= n_units
+    want = O.aggregate_unmask(p0[None, :], seeds, signs, L)
+    got = out[:L].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+
+
+def test_pair_units_bad_arguments(eng):
+    import torch
+    dev = torch.device("cuda:0")
+    ws = torch.zeros(4, dtype=torch.int32, device=dev)
+    out = torch.zeros(1024, dtype=torch.int32, device=dev)
+    seeds = torch.zeros((4, 32), dtype=torch.uint8, device=dev)
+    signs = torch.ones(4, dtype=torch.int8, device=dev)
+    with pytest.raises(RuntimeError):
+        eng.pair_units_dev(seeds, signs, out, 1024, ws, groups=0)
+    with pytest.raises(RuntimeError):       # the final pass needs both partial rows
+        eng.pair_units_dev(seeds, signs, out, 1024, ws, groups=4, final=True)
+    with pytest.raises(RuntimeError):       # 16-byte alignment of the final pass's rows
+        eng.pair_units_dev(seeds, signs, out[1:], 1000, ws, groups=4, p0=out[:1000], p1=out[:1000], final=True)

@@ -1,6 +1,8 @@
 """c5-shaped server reconstruction, CU-partitioned, with the pair masks of the first f*L slots
 added on the EC CUs once the combine is done (ServerReconstruction pair_split): sweep EC CU
-count x f.  Prints one line per case with the mean of 6 runs and the out == |U| check."""
+count x f.  f = "q" is the dynamic split instead (pair_queue: the EC CUs claim pair-mask units
+until the self-mask pass ends).  CU_PICK = first | stride.  Prints one line per case with the
+mean of 6 runs and the out == |U| check."""
 import os
 import sys
 
@@ -28,10 +30,12 @@ del rows
 t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
-cases = [(int(c), float(f)) for c in os.environ.get("EC_CUS", "24,32,40").split(",")
+cases = [(int(c), f) for c in os.environ.get("EC_CUS", "24,32,40").split(",")
          for f in os.environ.get("SPLIT", "0,0.2,0.35,0.5").split(",")]
 for ec_cus, f in cases:
-    rec = ServerReconstruction(eng, pass1_min_items=4096, ec_cus=ec_cus, cu_pick="first", pair_split=f)
+    q = f == "q"
+    rec = ServerReconstruction(eng, pass1_min_items=4096, ec_cus=ec_cus, cu_pick=os.environ.get("CU_PICK", "first"),
+                               pair_split=0.0 if q else float(f), pair_queue=q)
     args = (r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out)
     with torch.cuda.stream(main):
         for _ in range(2):
@@ -44,4 +48,4 @@ for ec_cus, f in cases:
     torch.cuda.synchronize()
     ok = bool(torch.all(out == len(on)).item())
     rec.close()
-    print(f"ec_cus={ec_cus} pair_split={f:.2f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
+    print(f"ec_cus={ec_cus} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)

@@ -1,5 +1,7 @@
 """c5-shaped reconstruction with the CU-split schedule, a few rounds, for rocprofv3 --kernel-trace:
-the timeline of pass 1 (Shamir + self-mask unmask), the EC combine and pass 2 (pair masks)."""
+the timeline of pass 1 (Shamir + self-mask unmask), the EC combine and pass 2 (pair masks).
+QUEUE=1: the pair_queue schedule, then the pair masks alone once through the work queue
+(pair_units_kernel) and once through items_kernel, to compare the two kernels."""
 import os
 import sys
 
@@ -29,9 +31,25 @@ del rows
 t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
-rec = ServerReconstruction(eng, pass1_min_items=MIN_ITEMS, ec_cus=EC_CUS, cu_pick="first")
+QUEUE = os.environ.get("QUEUE", "0") == "1"
+rec = ServerReconstruction(eng, pass1_min_items=MIN_ITEMS, ec_cus=EC_CUS, cu_pick="first", pair_queue=QUEUE)
 with torch.cuda.stream(main):
     for _ in range(4):
         rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out, stream=main)
         torch.cuda.synchronize()
 print("correct", bool(torch.all(out == len(on)).item()), flush=True)
+if QUEUE:
+    D = R["c1"].shape[0]
+    p_seeds = rec._bufs["seeds"][len(on):]
+    ws = rec._bufs["ws"]
+    print("units claimed by the side pass (last round): see the trace; total units",
+          ((L + 1023) // 1024) * ((D + 15) // 16), flush=True)
+    zero = torch.zeros((2, L), dtype=torch.int32, device=dev)
+    for _ in range(3):
+        ws.zero_()
+        eng.flag_set_dev(ws)
+        rec.side_eng.pair_units_dev(p_seeds, t["pair_signs"], out, L, ws, eng.cu_count() * 32, p0=zero[0], p1=zero[1],
+                                    final=True)
+        eng.aggregate_unmask_dev(None, p_seeds, t["pair_signs"], zero[1], L=L)
+    torch.cuda.synchronize()
+rec.close()
