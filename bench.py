@@ -209,7 +209,9 @@ def main():
         "config": {"workload": "c4: aggregate + self-mask and dropout-pair unmask, one server round",
                    "clients": N, "clients_per_gpu": Ng, "online": int(len(online)), "L": L, "seeds_K": int(K),
                    "dropout_pairs_D": int(D),
-                   "parallelism": f"client-shard{G}+slot-shard{G}" + ("+rccl-reduce-scatter-overlapped" if G > 1 else "")},
+                   "parallelism": f"client-shard{G}+slot-shard{G}" + (
+                       f"+{'rccl' if args.dist_backend == 'nccl' else args.dist_backend}-reduce-scatter-overlapped"
+                       if G > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "items_kernel<1>", "kernel_ms": round(kms, 4),
