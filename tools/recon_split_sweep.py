@@ -32,7 +32,12 @@ out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
 cases = [(int(c), f) for c in os.environ.get("EC_CUS", "24,32,40").split(",")
          for f in os.environ.get("SPLIT", "0,0.2,0.35,0.5").split(",")]
-for ec_cus, f in cases:
+# EC_TUNE="threads:waves,..." (flm_set_tuning ec_threads / ec_waves) multiplies the cases
+tunes = [tuple(int(v) for v in x.split(":")) for x in os.environ.get("EC_TUNE", "64:1").split(",")]
+cases = [(c, f, tn) for tn in tunes for c, f in cases]
+for ec_cus, f, (ec_threads, ec_waves) in cases:
+    eng.set_tuning("ec_threads", ec_threads)
+    eng.set_tuning("ec_waves", ec_waves)
     q = f == "q"
     rec = ServerReconstruction(eng, pass1_min_items=4096, ec_cus=ec_cus, cu_pick=os.environ.get("CU_PICK", "first"),
                                pair_split=0.0 if q else float(f), pair_queue=q)
@@ -48,4 +53,4 @@ for ec_cus, f in cases:
     torch.cuda.synchronize()
     ok = bool(torch.all(out == len(on)).item())
     rec.close()
-    print(f"ec_cus={ec_cus} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
+    print(f"ec_cus={ec_cus} ec_threads={ec_threads} ec_waves={ec_waves} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
