@@ -71,7 +71,8 @@ def worker(rank, world, port, N, K, L, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N,K,L", [(2, 6, 5, 5000), (2, 3, 0, 2048), (3, 7, 9, 4100), (4, 9, 11, 6000)])
+@pytest.mark.parametrize("world,N,K,L", [(2, 6, 5, 5000), (2, 3, 0, 2048), (3, 7, 9, 4100), (4, 9, 11, 6000),
+                                          (8, 13, 7, 9000)])  # G=8: ranks 5-7 own empty slot shards
 def test_sharded_round_matches_single_process(world, N, K, L):
     rows, seeds, signs = case(N, K, L)
     want = O.aggregate_unmask(rows, seeds, signs, threads=4)
