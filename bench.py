@@ -34,11 +34,13 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident aggregate+unmask GB/s, N clients × L int32 per round"
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 Tops/s
-# Measured ChaCha20 ceiling of the chip: a memory-free ChaCha kernel, compiler or hand-scheduled
-# asm, runs 612-645 G words/s (profiles/r01_chacha_probe.log, r01_chacha_{asm,full}_probe.log):
-# every ChaCha instruction costs ~3.9 cycles, so the 2-cycle simple-op rate behind VALU_PEAK_TOPS
-# is not reachable for this dependency graph.
-CHACHA_CEILING_GWORDS = 640.0
+# Measured ChaCha20 ceiling of the chip.  v_add_u32 / v_xor_b32 issue in ~2.1 cycles per wave
+# instruction on gfx950, v_alignbit_b32 (the rotate) in ~4.1.  Quarter-round streams with the four
+# QRs of a half round in lockstep (every step for all four QRs back to back) run at 3.52 cycles per
+# instruction (profiles/r01_issue_probe.log, QR8); compiler-scheduled ChaCha ran at ~4.0 (612-645
+# G words/s, profiles/r01_chacha_probe.log).  At 3.52 cycles, 60.4 instructions per word and 2.38
+# GHz: 256 CU x 4 SIMD x 64 lanes x 2.38e9 / 3.52 / 60.4 = 733 G words/s.
+CHACHA_CEILING_GWORDS = 733.0
 CHACHA_OPS_PER_WORD = 60.4       # VALU instructions per mask word in items_kernel (.s count)
 
 
@@ -223,7 +225,7 @@ def main():
                           "mask_gwords_per_s": round(words / (kms * 1e-3) / 1e9, 1),
                           "measured_chacha_ceiling_gwords": CHACHA_CEILING_GWORDS,
                           "frac_of_measured_ceiling": round(words / (kms * 1e-3) / 1e9 / CHACHA_CEILING_GWORDS, 4),
-                          "ceiling_source": "profiles/r01_chacha_probe.log, r01_chacha_asm_probe.log"},
+                          "ceiling_source": "profiles/r01_issue_probe.log (QR8 lockstep: 3.52 cycles per instruction)"},
     }
 
     tr = committed_traffic(rows_rank, L, int(K))

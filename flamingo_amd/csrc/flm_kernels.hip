@@ -39,6 +39,29 @@ namespace flm {
     a += b; d ^= a; d = FLM_ROTL(d, 8);           \
     c += d; b ^= c; b = FLM_ROTL(b, 7);
 
+// Rounds 2..10 as inline asm, the four quarter rounds of a half round in lockstep: each of the
+// QR's 12 steps issues for all four QRs back to back (4 adds, 4 xors, 4 rotates, ...).  gfx950
+// issues v_add_u32 / v_xor_b32 in about 2 cycles and v_alignbit_b32 in about 4; left to the
+// compiler, the rotates land between the adds and xors and the whole stream runs at ~4.0 cycles
+// per instruction.  Grouped like this, QR streams measured 3.52 (tools/issue_probe.hip,
+// profiles/r01_issue_probe.log).  One asm statement per instruction, volatile so the order holds.
+#define FLM_A(x, y) asm volatile("v_add_u32 %0, %1, %0" : "+v"(x) : "v"(y))
+#define FLM_X(x, y) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x) : "v"(y))
+#define FLM_R(x, s) asm volatile("v_alignbit_b32 %0, %0, %0, " #s : "+v"(x))  // rotl(x, 32 - s)
+#define FLM_QR4(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3)               \
+    FLM_A(a0, b0); FLM_A(a1, b1); FLM_A(a2, b2); FLM_A(a3, b3);                             \
+    FLM_X(d0, a0); FLM_X(d1, a1); FLM_X(d2, a2); FLM_X(d3, a3);                             \
+    FLM_R(d0, 16); FLM_R(d1, 16); FLM_R(d2, 16); FLM_R(d3, 16);                             \
+    FLM_A(c0, d0); FLM_A(c1, d1); FLM_A(c2, d2); FLM_A(c3, d3);                             \
+    FLM_X(b0, c0); FLM_X(b1, c1); FLM_X(b2, c2); FLM_X(b3, c3);                             \
+    FLM_R(b0, 20); FLM_R(b1, 20); FLM_R(b2, 20); FLM_R(b3, 20);                             \
+    FLM_A(a0, b0); FLM_A(a1, b1); FLM_A(a2, b2); FLM_A(a3, b3);                             \
+    FLM_X(d0, a0); FLM_X(d1, a1); FLM_X(d2, a2); FLM_X(d3, a3);                             \
+    FLM_R(d0, 24); FLM_R(d1, 24); FLM_R(d2, 24); FLM_R(d3, 24);                             \
+    FLM_A(c0, d0); FLM_A(c1, d1); FLM_A(c2, d2); FLM_A(c3, d3);                             \
+    FLM_X(b0, c0); FLM_X(b1, c1); FLM_X(b2, c2); FLM_X(b3, c3);                             \
+    FLM_R(b0, 25); FLM_R(b1, 25); FLM_R(b2, 25); FLM_R(b3, 25);
+
 // ------------------------------------------------------------------ seeds
 // One thread per seed builds its SeedRec from the raw 32 seed bytes and sign.
 // Workgroup p writes its count of negative / invalid signs to meta[2+2p],
@@ -153,6 +176,7 @@ __device__ __forceinline__ void chacha_mask_add(const SeedRec *__restrict__ rec,
     x8 += x13; x7 ^= x8; x7 = FLM_ROTL(x7, 7);
     FLM_QR(x3, x4, x9, x14);
     // rounds 2..10
+#ifdef FLM_COMPILER_QR
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
         FLM_QR(x0, x4, x8, x12);
@@ -164,6 +188,13 @@ __device__ __forceinline__ void chacha_mask_add(const SeedRec *__restrict__ rec,
         FLM_QR(x2, x7, x8, x13);
         FLM_QR(x3, x4, x9, x14);
     }
+#else
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        FLM_QR4(x0, x4, x8, x12, x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15);
+        FLM_QR4(x0, x5, x10, x15, x1, x6, x11, x12, x2, x7, x8, x13, x3, x4, x9, x14);
+    }
+#endif
     // feed-forward (input words 13..15 are zero), fold "abcd"/sign, accumulate
     m[0] += (x0 + kSigma0) ^ xc;
     m[1] += (x1 + kSigma1) ^ xc;
