@@ -262,6 +262,8 @@ def main():
 RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-split schedule (recon_probe sweep:
                           # 24 of MI355X's 256); a multiple of the 8 XCDs so every XCD loses the same count
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
+RECON_QUEUE_MIN_ITEMS = 1024  # its pass 1 plan: single-tile items, the 57-VGPR merged variant at 8 waves/SIMD
+                             # (8.94 ms vs 9.08 at 4096 and 9.42 at 2048; profiles/r01_recon_queue_minitems.log)
 RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 24 / 32 / 40 CUs ->
                                 # 9.97 / 9.75 / 11.05 ms at c5; profiles/r01_recon_queue_sweep.log)
 
@@ -292,8 +294,8 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
                                         cu_pick="first")
         q_cus = max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count() / 8)) * 8) if eng.cu_count() >= 64 else \
             max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count())))
-        recon_q = ServerReconstruction(eng, dev, pass1_min_items=RECON_MIN_ITEMS, ec_cus=q_cus, cu_pick="first",
-                                       pair_queue=True)
+        recon_q = ServerReconstruction(eng, dev, pass1_min_items=RECON_QUEUE_MIN_ITEMS, ec_cus=q_cus,
+                                       cu_pick="first", pair_queue=True)
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         n_off = int(round(dropout * N))
