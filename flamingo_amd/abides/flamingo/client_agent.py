@@ -144,7 +144,7 @@ class SA_ClientAgent(Agent):
             return
         self.neighbors_list = param.find_neighbors(param.root_seed, self.current_iteration, self.num_clients,
                                                    self.id, self.neighborhood_size)
-        nb = sorted(self.neighbors_list)
+        nb = list(self.neighbors_list)          # the reference's set order (:256, :295, :330)
         if self.id in self.neighbors_list:
             raise RuntimeError("id itself appears in its neighbor list")
         committee = sorted(self.user_committee)

@@ -172,7 +172,7 @@ def elgamal_masks(agent, iteration: int, nb: list):
             c = _clients[cid]
             if iteration in c.offline_iterations or (root_seed, iteration, cid) in _elgamal:
                 continue
-            cnb = sorted(neighbors(iteration, c.num_clients, c.neighborhood_size)[cid])
+            cnb = list(neighbors(iteration, c.num_clients, c.neighborhood_size)[cid])
             batch.append((cid, [c._rand_scalar() for _ in cnb]))
         if agent.id not in [b[0] for b in batch]:
             batch.append((agent.id, [agent._rand_scalar() for _ in nb]))

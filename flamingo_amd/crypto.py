@@ -14,10 +14,13 @@ binds the same primitives from OpenSSL's libcrypto through ctypes:
   SA_ClientAgent.py:236-241 / :423-425;
 * ECDSA-SHA256 signatures (DSS 'fips-186-3', SA_ServiceAgent.py:382-386).
 
-PARITY NOTE: map_to_curve takes `next(libnum.sqrtmod(...))` (ecchash.py:263-268);
-libnum's root order is not available here, so this module picks the root
-y <= p - y.  Client and server use the same function, so masks still cancel;
-s_ij values are not claimed equal to the reference's (parity unpinned).
+PARITY NOTE: map_to_curve takes `next(libnum.sqrtmod(...))` (ecchash.py:263-268).
+libnum is absent, so its root order cannot be observed; this module takes the
+direct root a^((p+1)/4) mod p first (p = 3 mod 4), which is what libnum's
+sqrtmod_prime_power computes before yielding p - root.  With that one
+convention assumed, the whole pair-seed pipeline (ECDH -> SHA-256 -> h_ijt ->
+hash-to-curve -> SHA-256) reproduces the s_ij the reference's own
+SA_ClientAgent.sendVectors produced (tests/test_ref_golden_cpu.py).
 """
 from __future__ import annotations
 
@@ -218,10 +221,10 @@ def hash_to_field(msg: bytes, count: int, modulus: int, blen: int = 48):
 
 
 def _sqrt(v: int):
-    r = pow(v, (P + 1) // 4, P)          # P = 3 mod 4
+    r = pow(v, (P + 1) // 4, P)          # P = 3 mod 4: the root libnum yields first
     if r * r % P != v % P:
         return None
-    return min(r, P - r)
+    return r
 
 
 def map_to_curve(u: int):

@@ -374,15 +374,18 @@ int run_small_round(flm_ctx *ctx, int B, const uint32_t *d_rows, uint64_t pitch,
     return 0;
 }
 
-// zero_out (optional): the round's output, zero-filled by the same launch (zero_n words)
+// zero_out (optional): the round's output, zero-filled by the same launch (zero_n words).
+// Only flm_seed_table_dev publishes the table for a later flm_aggregate_dev (publish = true); every
+// other entry point that rebuilds it (prg expansion, client masking, pair units, the fused round)
+// invalidates it, so aggregate_dev can never unmask against seeds it was not given.
 int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s,
-                      uint32_t *zero_out = nullptr, uint64_t zero_n = 0) {
+                      uint32_t *zero_out = nullptr, uint64_t zero_n = 0, bool publish = false) {
     FLM_HIP(ctx, ctx->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec)));
     const int groups = flm::seed_schedule_groups(K, zero_out ? zero_n : 0);
     FLM_HIP(ctx, ctx->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)groups)));
     FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s,
                                            zero_out, zero_n));
-    ctx->table_k = K;
+    ctx->table_k = publish ? K : -1;
     return 0;
 }
 
@@ -687,7 +690,7 @@ int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
-    return run_seed_schedule(ctx, d_seeds, d_signs, K, s);
+    return run_seed_schedule(ctx, d_seeds, d_signs, K, s, nullptr, 0, /*publish=*/true);
 }
 
 int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,

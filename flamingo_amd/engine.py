@@ -229,6 +229,8 @@ class MaskEngine:
         if mask_hi is None:
             mask_hi = L
         K = seeds.shape[0] if seeds is not None else 0
+        if K and (seeds.shape[-1] != 32 or signs.shape[0] < K):
+            raise RuntimeError(f"seeds must be (K, 32) with >= K signs, got {tuple(seeds.shape)}, {tuple(signs.shape)}")
         # plain ints for the c_void_p arguments: this call is the whole host cost of a small
         # round (c2: ~6.5 us of GPU time), so no per-call ctypes wrapper objects
         rc = self.lib.flm_aggregate_unmask_dev(
@@ -284,6 +286,20 @@ class MaskEngine:
         seg = np.ascontiguousarray(seg, dtype=np.int64)
         N = seg.shape[0] - 1
         signs = np.ascontiguousarray(signs, dtype=np.int8)
+        K = int(seg[-1]) if N >= 0 else 0
+        # the C side reads signs[0..seg[N]) from this host array and indexes the device seed
+        # table by seg: check both here, where the shapes are known
+        if N < 0 or seg[0] != 0 or np.any(np.diff(seg) < 0):
+            raise RuntimeError("seg must be non-decreasing from 0")
+        if signs.ndim != 1 or signs.shape[0] != K:
+            raise RuntimeError(f"{signs.shape[0] if signs.ndim else 0} signs for seg[-1] = {K} seeds")
+        if K and (seeds_dev.dim() != 2 or seeds_dev.shape[1] != 32 or seeds_dev.element_size() != 1
+                  or seeds_dev.shape[0] < K):
+            raise RuntimeError(f"seeds_dev must be a (>= {K}, 32) uint8 tensor, got {tuple(seeds_dev.shape)}")
+        if out.dim() != 2 or out.shape[0] < N or out.element_size() != 4 or out.shape[1] < L:
+            raise RuntimeError(f"out must be (>= {N}, >= {L}) 32-bit, got {tuple(out.shape)}")
+        if x is not None and (tuple(x.shape) != tuple(out.shape) or x.element_size() != 4):
+            raise RuntimeError("x must have out's shape and a 32-bit dtype")
         pitch = out.shape[1]
         rc = self.lib.flm_client_mask_dev(self.ctx, ctypes.c_void_p(x.data_ptr() if x is not None else 0), pitch, N,
                                           p_i64(seg), ctypes.c_void_p(seeds_dev.data_ptr()), p_i8(signs), L,

@@ -82,14 +82,27 @@ def chosen_table(root_seed: bytes, iteration: int, num_clients: int, neighborhoo
 
 def neighbor_graph(root_seed: bytes, iteration: int, num_clients: int, neighborhood_size: int,
                    encrypt=None) -> list:
-    """findNeighbors for every client at once: N(i) = chosen(i) \\ {i}  U  {j != i : i in chosen(j)}."""
-    ch = chosen_table(root_seed, iteration, num_clients, neighborhood_size, encrypt)
-    nbrs = [set() for _ in range(num_clients)]
+    """findNeighbors for every client at once: N(i) = chosen(i) \\ {i}  U  {j != i : i in chosen(j)}.
+
+    Each set is built with the reference's insertion sequence -- its own draws in
+    draw order (util/param.py:83-91), then the choosers in ascending id (:95-101) --
+    so that iterating it gives the reference's set order, which fixes the order of
+    dec_target_pairwise / recon_symbol on the server (SA_ServiceAgent.py:360-378)."""
+    ch = chosen_table(root_seed, iteration, num_clients, neighborhood_size, encrypt).tolist()
+    choosers = [[] for _ in range(num_clients)]
     for i in range(num_clients):
-        for t in ch[i].tolist():
+        for t in ch[i]:
             if t != i:
-                nbrs[i].add(t)
-                nbrs[t].add(i)   # i chose t  =>  i is in t's list of choosers (:95-101)
+                choosers[t].append(i)       # i chose t: i is in t's list of choosers
+    nbrs = []
+    for i in range(num_clients):
+        s = set()
+        for t in ch[i]:
+            if t != i:
+                s.add(t)
+        for j in choosers[i]:               # ascending: appended in increasing i
+            s.add(j)
+        nbrs.append(s)
     return nbrs
 
 
@@ -99,14 +112,21 @@ def find_neighbors(root_seed: bytes, current_iteration: int, num_clients: int, i
     return neighbor_graph(root_seed, current_iteration, num_clients, neighborhood_size, encrypt)[id]
 
 
-def dropout_pairs(nbrs: list, online, offline):
-    """SA_ServiceAgent.report_process (:359-380): (online nb, offline id) pairs and recon_symbol.
+def dropout_pairs(nbrs: list, online, offline, users=None):
+    """SA_ServiceAgent.report_process (:341-380): (online nb, offline id) pairs and recon_symbol.
 
-    Offline ids in set iteration order, then each one's neighbours in set
-    order -- the reference's insertion order of dec_target_pairwise."""
+    The offline set is formed as the reference forms it, ``set(users) - set(online)``
+    (users defaults to range(N), config/flamingo.py:208), and walked in that set's
+    iteration order, each offline id's neighbours in the order of their set -- the
+    reference's insertion order of dec_target_pairwise.  Pinned against the
+    reference's own recon_symbol in tests/test_ref_golden_cpu.py."""
     online_s = set(int(i) for i in online)
+    users = range(len(nbrs)) if users is None else users
+    want = set(int(j) for j in offline)
     pairs, signs = [], []
-    for cid in set(int(j) for j in offline):
+    for cid in set(users) - online_s:
+        if cid not in want:
+            continue
         for nb in nbrs[cid]:
             if nb in online_s:
                 if nb == cid:

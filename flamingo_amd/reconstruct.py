@@ -113,38 +113,44 @@ class ServerReconstruction:
         main = torch.cuda.current_stream(self.device) if stream is None else stream
         M = mi_shares.shape[1]
         D = c1.shape[0] if c1 is not None else 0
-        seeds = self._buf("seeds", (M + D, 32), torch.uint8)
-        flags = self._buf("flags", (max(D, 1),), torch.int32)
+        # Every buffer (and every fill) is made on the caller's stream BEFORE the `ready`
+        # event below, so the side and CU-partitioned streams that wait on `ready` see it
+        # initialised, on the first run and whenever a shape changes.
+        with torch.cuda.stream(main):
+            seeds = self._buf("seeds", (M + D, 32), torch.uint8)
+            flags = self._buf("flags", (max(D, 1),), torch.int32)
+            neg = self._buf("neg", (M,), torch.int8, -1)
+            if D and not overlap:
+                signs = self._buf("signs_all", (M + D,), torch.int8)
+                signs[:M].fill_(-1)
+                signs[M:].copy_(pair_signs)
         m_seeds, p_seeds = seeds[:M], seeds[M:]
         if D == 0:
             eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
-            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), out, L=L, stream=main)
+            eng.aggregate_unmask_dev(rows, m_seeds, neg, out, L=L, stream=main)
             return out, flags[:0]
         if not overlap:
-            signs = self._buf("signs_all", (M + D,), torch.int8)
-            signs[:M].fill_(-1)
-            signs[M:].copy_(pair_signs)
             eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
             eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=main)
             eng.aggregate_unmask_dev(rows, seeds, signs, out, L=L, stream=main)
             return out, flags
         if self.pair_queue:
             return self._run_queue(rows, L, lambdas, mi_shares, c1, pair_shares, pair_signs, out, main,
-                                   m_seeds, p_seeds, flags)
+                                   m_seeds, p_seeds, flags, neg)
+        caller = main
+        with torch.cuda.stream(caller):
+            part = self._buf("tmp", (2 if self.pair_split else 1, rows.shape[1]), torch.int32)
         ready = torch.cuda.Event()
         ready.record(main)                       # inputs enqueued on main are visible to the side stream
         self.side.wait_event(ready)
         eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
         done = torch.cuda.Event()
         done.record(self.side)
-        caller = main
         if self.part is not None:
             self.part.wait_event(ready)
             main = self.part
         eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
-        pitch = rows.shape[1]
         # part[0]: rows + self masks; part[1]: the side stream's share of the pair masks
-        part = self._buf("tmp", (2 if self.pair_split else 1, pitch), torch.int32)
         tmp = part[:1]
         lo = int(self.pair_split * L) // 1024 * 1024 if self.pair_split else 0
         if lo:
@@ -155,8 +161,7 @@ class ServerReconstruction:
         if self.pass1_min_items != 1024:
             eng.set_tuning("min_items", self.pass1_min_items)
         try:
-            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (M,), torch.int8, -1), tmp[0], L=L,
-                                     stream=main)
+            eng.aggregate_unmask_dev(rows, m_seeds, neg, tmp[0], L=L, stream=main)
         finally:
             if self.pass1_min_items != 1024:
                 eng.set_tuning("min_items", 1024)
@@ -175,12 +180,12 @@ class ServerReconstruction:
 
 
     def _run_queue(self, rows, L, lambdas, mi_shares, c1, pair_shares, pair_signs, out, caller, m_seeds, p_seeds,
-                   flags):
+                   flags, neg):
         eng, side_eng = self.eng, self.side_eng
         pitch = rows.shape[1]
-        part = self._buf("tmp", (2, pitch), torch.int32)
-        ws = self._buf("ws", (4,), torch.int32)
         with torch.cuda.stream(caller):
+            part = self._buf("tmp", (2, pitch), torch.int32)
+            ws = self._buf("ws", (4,), torch.int32)
             ws.zero_()                           # unit counter, stop flag
             part[1].zero_()                      # the side pass adds into it
         ready = torch.cuda.Event()
@@ -196,8 +201,7 @@ class ServerReconstruction:
         if self.pass1_min_items != 1024:
             eng.set_tuning("min_items", self.pass1_min_items)
         try:
-            eng.aggregate_unmask_dev(rows, m_seeds, self._buf("neg", (m_seeds.shape[0],), torch.int8, -1), part[0],
-                                     L=L, stream=self.part)
+            eng.aggregate_unmask_dev(rows, m_seeds, neg, part[0], L=L, stream=self.part)
         finally:
             if self.pass1_min_items != 1024:
                 eng.set_tuning("min_items", 1024)
