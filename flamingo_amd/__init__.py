@@ -8,6 +8,6 @@ The package holds what the path needs and nothing else:
   distributed  the multi-GPU round (client-sharded rows, RCCL reduce-scatter)
   abides/    the ABIDES Kernel/Agent/Message surface and the Flamingo agents
 """
-from .engine import MaskEngine, PinnedArena  # noqa: F401
+from .engine import DeviceGroup, MaskEngine, PinnedArena  # noqa: F401
 
-__all__ = ["MaskEngine", "PinnedArena"]
+__all__ = ["DeviceGroup", "MaskEngine", "PinnedArena"]

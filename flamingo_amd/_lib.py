@@ -56,6 +56,24 @@ SIGNATURES = {
     "flm_cu_count": (_int, [_vp, _vp]),
     "flm_stream_create_cu_mask": (_int, [_vp, _vp, _int, _vp]),
     "flm_stream_destroy": (_int, [_vp, _vp]),
+    "flm_shard_bounds": (_int, [_sz, _int, _int, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    "flm_client_bounds": (_int, [_int, _int, _int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "flm_comm_unique_id": (_int, [_vp]),
+    "flm_comm_init_rank": (_int, [_vp, _int, _int, _vp]),
+    "flm_comm_size": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "flm_reduce_scatter_dev": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "flm_all_gather_dev": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "flm_group_init": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int)]),
+    "flm_group_free": (None, [_vp]),
+    "flm_group_last_error": (ctypes.c_char_p, [_vp]),
+    "flm_group_size": (_int, [_vp]),
+    "flm_group_is_loopback": (_int, [_vp]),
+    "flm_group_ctx": (_vp, [_vp, _int]),
+    "flm_group_sync": (_int, [_vp]),
+    "flm_group_aggregate_unmask": (_int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),
+    "flm_group_aggregate_unmask_dev": (_int, [_vp, ctypes.POINTER(_vp), _sz, ctypes.POINTER(_int),
+                                              ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _sz,
+                                              ctypes.POINTER(_vp)]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }

@@ -1,0 +1,473 @@
+// flm_comm.hip -- RCCL over xGMI for the multi-GPU server round.
+//
+// The reference server is one single-threaded discrete-event process
+// (Kernel.py:190-271); its partial sum and unmask (SA_ServiceAgent.py:346-350,
+// 529-605) are one vector of L uint32.  On G GPUs the work shards two ways:
+//   * rows by client: rank r ingests clients [N*r/G, N*(r+1)/G) over its own link
+//     and sums them over all L slots;
+//   * masks by slot: rank r regenerates every seed's mask over its own shard
+//     [r*S, (r+1)*S) only, S = round_up(L, 1024*G) / G (the VALU-bound part);
+// then ONE reduce-scatter (ncclUint32, ncclSum: mod 2^32, so any ring order gives
+// the same bits) returns each rank its shard of S + C + M.
+//
+// Two ways to drive it:
+//   * one process per GPU (torchrun): each process attaches a communicator to its
+//     context (flm_comm_init_rank) and calls flm_reduce_scatter_dev on its partial;
+//   * one process for all GPUs (the drop-in DES server): flm_group owns one context
+//     per device plus a communicator clique (ncclCommInitAll), and
+//     flm_group_aggregate_unmask runs the whole round from host rows.
+//
+// RCCL is resolved at run time (dlopen) so the library links against no RCCL:
+// the copy already loaded in the process (PyTorch's, which matches the HIP runtime
+// PyTorch loaded) is preferred, else /opt/rocm's librccl.so.1.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/flamingo_hip.h"
+#include "flm_internal.h"
+
+namespace {
+
+struct Rccl {
+    void *h = nullptr;
+    std::string err;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*ReduceScatter)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                  hipStream_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+Rccl *rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char *env = getenv("FLM_RCCL_LIBRARY");
+        const char *names[] = {"librccl.so", "librccl.so.1"};
+        if (env && *env) r.h = dlopen(env, RTLD_NOW | RTLD_GLOBAL);
+        for (const char *n : names)  // a copy some other library (PyTorch) already loaded
+            if (!r.h) r.h = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+        if (!r.h) r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!r.h) {
+            r.err = std::string("cannot load RCCL: ") + dlerror();
+            return;
+        }
+#define FLM_SYM(field, name)                                                   \
+    r.field = reinterpret_cast<decltype(r.field)>(dlsym(r.h, name));           \
+    if (!r.field) {                                                            \
+        r.err = std::string("RCCL symbol missing: ") + name;                   \
+        r.h = nullptr;                                                         \
+        return;                                                                \
+    }
+        FLM_SYM(GetUniqueId, "ncclGetUniqueId");
+        FLM_SYM(CommInitRank, "ncclCommInitRank");
+        FLM_SYM(CommInitAll, "ncclCommInitAll");
+        FLM_SYM(CommDestroy, "ncclCommDestroy");
+        FLM_SYM(ReduceScatter, "ncclReduceScatter");
+        FLM_SYM(AllGather, "ncclAllGather");
+        FLM_SYM(GroupStart, "ncclGroupStart");
+        FLM_SYM(GroupEnd, "ncclGroupEnd");
+        FLM_SYM(GetErrorString, "ncclGetErrorString");
+#undef FLM_SYM
+    });
+    return r.h ? &r : nullptr;
+}
+
+struct CommState {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+CommState *comm_of(flm_ctx *ctx) { return static_cast<CommState *>(*flm::rt::comm_slot(ctx)); }
+
+int fail_ctx(flm_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail_ctx(flm_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return flm::rt::set_error(ctx, code, buf);
+}
+
+int rccl_missing(flm_ctx *ctx) {
+    return fail_ctx(ctx, FLM_EHIP, "RCCL unavailable (set FLM_RCCL_LIBRARY to librccl.so's path)");
+}
+
+#define FLM_NCCL(ctx, expr)                                                                           \
+    do {                                                                                              \
+        ncclResult_t r_ = (expr);                                                                     \
+        if (r_ != ncclSuccess)                                                                        \
+            return fail_ctx((ctx), FLM_EHIP, "%s failed: %s", #expr, rccl()->GetErrorString(r_));    \
+    } while (0)
+
+#define FLM_HIPC(ctx, expr)                                                                           \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) return fail_ctx((ctx), FLM_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+}  // namespace
+
+namespace flm {
+void comm_release(flm_ctx *ctx) {
+    CommState *cs = comm_of(ctx);
+    if (!cs) return;
+    if (cs->comm && rccl()) (void)rccl()->CommDestroy(cs->comm);
+    delete cs;
+    *flm::rt::comm_slot(ctx) = nullptr;
+}
+}  // namespace flm
+
+// =========================================================== shard geometry
+namespace {
+constexpr uint64_t kShardAlign = 1024;  // one wave's sub-tile: every shard start is a multiple of 16 slots
+
+uint64_t padded_len(uint64_t L, int G) {
+    const uint64_t q = kShardAlign * (uint64_t)G;
+    return (L + q - 1) / q * q;
+}
+}  // namespace
+
+extern "C" {
+
+int flm_shard_bounds(size_t L, int n_ranks, int rank, size_t *lo, size_t *hi, size_t *shard_words) {
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks || !lo || !hi) return FLM_EINVAL;
+    const uint64_t S = padded_len(L, n_ranks) / n_ranks;
+    *lo = (size_t)std::min<uint64_t>((uint64_t)rank * S, L);
+    *hi = (size_t)std::min<uint64_t>((uint64_t)(rank + 1) * S, L);
+    if (shard_words) *shard_words = (size_t)S;
+    return 0;
+}
+
+int flm_client_bounds(int N, int n_ranks, int rank, int *c0, int *c1) {
+    if (N < 0 || n_ranks < 1 || rank < 0 || rank >= n_ranks || !c0 || !c1) return FLM_EINVAL;
+    *c0 = (int)((int64_t)N * rank / n_ranks);
+    *c1 = (int)((int64_t)N * (rank + 1) / n_ranks);
+    return 0;
+}
+
+// ======================================================= one process per GPU
+int flm_comm_unique_id(uint8_t id_out[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
+    if (!id_out) return FLM_EINVAL;
+    Rccl *r = rccl();
+    if (!r) return flm::rt::set_error(nullptr, FLM_EHIP, "RCCL unavailable");
+    ncclUniqueId id;
+    ncclResult_t e = r->GetUniqueId(&id);
+    if (e != ncclSuccess) return flm::rt::set_error(nullptr, FLM_EHIP, r->GetErrorString(e));
+    std::memcpy(id_out, &id, sizeof id);
+    return 0;
+}
+
+int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128]) {
+    if (!ctx) return flm::rt::set_error(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks || !id) return fail_ctx(ctx, FLM_EINVAL, "bad rank %d of %d", rank, n_ranks);
+    Rccl *r = rccl();
+    if (!r) return rccl_missing(ctx);
+    flm::comm_release(ctx);
+    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    auto *cs = new CommState();
+    ncclResult_t e = r->CommInitRank(&cs->comm, n_ranks, uid, rank);
+    if (e != ncclSuccess) {
+        delete cs;
+        return fail_ctx(ctx, FLM_EHIP, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, r->GetErrorString(e));
+    }
+    cs->nranks = n_ranks;
+    cs->rank = rank;
+    *flm::rt::comm_slot(ctx) = cs;
+    return 0;
+}
+
+int flm_comm_size(flm_ctx *ctx, int *n_ranks, int *rank) {
+    if (!ctx || !n_ranks || !rank) return FLM_EINVAL;
+    CommState *cs = comm_of(ctx);
+    *n_ranks = cs ? cs->nranks : 1;
+    *rank = cs ? cs->rank : 0;
+    return cs ? 0 : 1;  // 1: no communicator attached
+}
+
+int flm_reduce_scatter_dev(flm_ctx *ctx, const uint32_t *d_send, uint32_t *d_recv, size_t recv_words, void *stream) {
+    if (!ctx) return flm::rt::set_error(nullptr, FLM_EINVAL, "ctx is NULL");
+    CommState *cs = comm_of(ctx);
+    if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
+    if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
+    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : flm::rt::stream_of(ctx);
+    FLM_NCCL(ctx, rccl()->ReduceScatter(d_send, d_recv, recv_words, ncclUint32, ncclSum, cs->comm, s));
+    return 0;
+}
+
+int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t send_bytes, void *stream) {
+    if (!ctx) return flm::rt::set_error(nullptr, FLM_EINVAL, "ctx is NULL");
+    CommState *cs = comm_of(ctx);
+    if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
+    if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
+    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : flm::rt::stream_of(ctx);
+    FLM_NCCL(ctx, rccl()->AllGather(d_send, d_recv, send_bytes, ncclUint8, cs->comm, s));
+    return 0;
+}
+
+}  // extern "C"
+
+// ======================================================= one process, G GPUs
+struct flm_group {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<flm_ctx *> ctx;
+    bool loopback = false;  // every rank on one device: exchange by shard_sum_kernel, no RCCL
+    struct Rank {
+        uint32_t *partial = nullptr, *shard = nullptr;
+        size_t cap_partial = 0, cap_shard = 0;
+        hipEvent_t done = nullptr;
+    };
+    std::vector<Rank> rk;
+    std::string err;
+};
+
+namespace {
+
+int gfail(flm_group *g, int code, const std::string &msg) {
+    if (g) g->err = msg;
+    flm::rt::set_error(nullptr, code, msg.c_str());
+    return code;
+}
+
+int grow(flm_group *g, int r, uint32_t *&p, size_t &cap, size_t words) {
+    if (words <= cap) return 0;
+    (void)hipSetDevice(g->dev[r]);
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(words, 64) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(p, 0, std::max<size_t>(words, 64) * sizeof(uint32_t));
+    if (e != hipSuccess) return gfail(g, FLM_ENOMEM, std::string("group buffer: ") + hipGetErrorString(e));
+    cap = words;
+    return 0;
+}
+
+int rank_error(flm_group *g, int r, int rc) {
+    return gfail(g, rc, "rank " + std::to_string(r) + ": " + flm_last_error(g->ctx[r]));
+}
+
+// The exchange: partial[r] (Lp words each) -> shards[r] (S words each), on each rank's stream.
+int exchange(flm_group *g, uint64_t S, const std::vector<uint32_t *> &shards) {
+    const int G = g->n;
+    if (g->loopback) {
+        std::vector<const uint32_t *> parts(G);
+        for (int r = 0; r < G; ++r) parts[r] = g->rk[r].partial;
+        for (int r = 0; r < G; ++r) {
+            hipStream_t s = flm::rt::stream_of(g->ctx[r]);
+            for (int q = 0; q < G; ++q)
+                if (q != r && hipStreamWaitEvent(s, g->rk[q].done, 0) != hipSuccess)
+                    return gfail(g, FLM_EHIP, "hipStreamWaitEvent");
+            hipError_t e = flm::launch_shard_sum(parts.data(), G, (uint64_t)r * S, S, shards[r], s);
+            if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("shard_sum: ") + hipGetErrorString(e));
+        }
+        return 0;
+    }
+    Rccl *rc = rccl();
+    ncclResult_t e = rc->GroupStart();
+    for (int r = 0; r < G && e == ncclSuccess; ++r)
+        e = rc->ReduceScatter(g->rk[r].partial, shards[r], S, ncclUint32, ncclSum, comm_of(g->ctx[r])->comm,
+                              flm::rt::stream_of(g->ctx[r]));
+    const ncclResult_t e2 = rc->GroupEnd();
+    if (e != ncclSuccess || e2 != ncclSuccess)
+        return gfail(g, FLM_EHIP, std::string("ncclReduceScatter: ") + rc->GetErrorString(e != ncclSuccess ? e : e2));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int flm_group_init(flm_group **out, int n, const int *devices) {
+    if (!out) return gfail(nullptr, FLM_EINVAL, "flm_group_init: out is NULL");
+    *out = nullptr;
+    if (n < 1 || n > flm::kMaxParts) return gfail(nullptr, FLM_EINVAL, "flm_group_init: n must be in [1, 16]");
+    auto *g = new flm_group();
+    g->n = n;
+    for (int r = 0; r < n; ++r) g->dev.push_back(devices ? devices[r] : r);
+    bool all_same = true, distinct = true;
+    for (int r = 0; r < n; ++r)
+        for (int q = 0; q < r; ++q) {
+            all_same &= g->dev[r] == g->dev[q];
+            distinct &= g->dev[r] != g->dev[q];
+        }
+    if (!distinct && !all_same) {
+        delete g;
+        return gfail(nullptr, FLM_EINVAL, "flm_group_init: devices must be all distinct (RCCL) or all equal (loopback)");
+    }
+    g->loopback = n > 1 && all_same;
+    g->rk.resize(n);
+    for (int r = 0; r < n; ++r) {
+        flm_ctx *c = nullptr;
+        if (int rc = flm_init(&c, g->dev[r])) {
+            std::string m = flm_last_error(nullptr);
+            flm_group_free(g);
+            return gfail(nullptr, rc, "flm_group_init: rank " + std::to_string(r) + ": " + m);
+        }
+        g->ctx.push_back(c);
+        (void)hipSetDevice(g->dev[r]);
+        if (hipEventCreateWithFlags(&g->rk[r].done, hipEventDisableTiming) != hipSuccess) {
+            flm_group_free(g);
+            return gfail(nullptr, FLM_EHIP, "flm_group_init: hipEventCreate");
+        }
+    }
+    if (!g->loopback) {
+        Rccl *r = rccl();
+        if (!r) {
+            flm_group_free(g);
+            return gfail(nullptr, FLM_EHIP, "flm_group_init: RCCL unavailable");
+        }
+        std::vector<ncclComm_t> comms(n);
+        ncclResult_t e = r->CommInitAll(comms.data(), n, g->dev.data());
+        if (e != ncclSuccess) {
+            flm_group_free(g);
+            return gfail(nullptr, FLM_EHIP, std::string("ncclCommInitAll: ") + r->GetErrorString(e));
+        }
+        for (int q = 0; q < n; ++q) {
+            auto *cs = new CommState();
+            cs->comm = comms[q];
+            cs->nranks = n;
+            cs->rank = q;
+            *flm::rt::comm_slot(g->ctx[q]) = cs;
+        }
+    }
+    *out = g;
+    return 0;
+}
+
+void flm_group_free(flm_group *g) {
+    if (!g) return;
+    for (int r = 0; r < (int)g->ctx.size(); ++r) {
+        (void)hipSetDevice(g->dev[r]);
+        (void)hipStreamSynchronize(flm::rt::stream_of(g->ctx[r]));
+        if (g->rk[r].partial) (void)hipFree(g->rk[r].partial);
+        if (g->rk[r].shard) (void)hipFree(g->rk[r].shard);
+        if (g->rk[r].done) (void)hipEventDestroy(g->rk[r].done);
+        flm_free(g->ctx[r]);
+    }
+    delete g;
+}
+
+const char *flm_group_last_error(const flm_group *g) { return g ? g->err.c_str() : flm_last_error(nullptr); }
+
+int flm_group_size(const flm_group *g) { return g ? g->n : 0; }
+
+int flm_group_is_loopback(const flm_group *g) { return g && g->loopback ? 1 : 0; }
+
+flm_ctx *flm_group_ctx(flm_group *g, int rank) {
+    if (!g || rank < 0 || rank >= g->n) return nullptr;
+    return g->ctx[rank];
+}
+
+int flm_group_sync(flm_group *g) {
+    if (!g) return FLM_EINVAL;
+    for (int r = 0; r < g->n; ++r) {
+        (void)hipSetDevice(g->dev[r]);
+        hipError_t e = hipStreamSynchronize(flm::rt::stream_of(g->ctx[r]));
+        if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("rank sync: ") + hipGetErrorString(e));
+    }
+    return 0;
+}
+
+// Host rows in, unmasked sum out, over every device of the group (the drop-in server's round,
+// SA_ServiceAgent.py:346-350 + 529-605): one host thread per device uploads that device's
+// clients and enqueues its fused round; then one reduce-scatter; then each shard comes back.
+int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N, const uint8_t *seeds,
+                               const int8_t *signs, int K, size_t L, uint32_t *out) {
+    if (!g) return gfail(nullptr, FLM_EINVAL, "group is NULL");
+    if (N < 0 || K < 0) return gfail(g, FLM_EINVAL, "negative N or K");
+    if (L == 0) return 0;
+    if (!out || (N > 0 && !rows) || (K > 0 && (!seeds || !signs))) return gfail(g, FLM_EINVAL, "NULL argument");
+    const int G = g->n;
+    const uint64_t Lp = padded_len(L, G), S = Lp / G;
+    for (int r = 0; r < G; ++r) {
+        if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
+        if (int rc = grow(g, r, g->rk[r].shard, g->rk[r].cap_shard, S)) return rc;
+    }
+    std::vector<int> rcs(G, 0);
+    auto work = [&](int r) {
+        int c0, c1;
+        size_t lo, hi;
+        flm_client_bounds(N, G, r, &c0, &c1);
+        flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
+        rcs[r] = flm::rt::host_round_async(g->ctx[r], rows ? rows + c0 : nullptr, c1 - c0, seeds, signs, K, L, lo, hi,
+                                           g->rk[r].partial);
+        if (!rcs[r] && hipEventRecord(g->rk[r].done, flm::rt::stream_of(g->ctx[r])) != hipSuccess) rcs[r] = FLM_EHIP;
+    };
+    if (G == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int r = 0; r < G; ++r) th.emplace_back(work, r);
+        for (auto &t : th) t.join();
+    }
+    for (int r = 0; r < G; ++r)
+        if (rcs[r]) return rank_error(g, r, rcs[r]);
+    std::vector<uint32_t *> shards(G);
+    for (int r = 0; r < G; ++r) shards[r] = g->rk[r].shard;
+    if (int rc = exchange(g, S, shards)) return rc;
+    for (int r = 0; r < G; ++r) {
+        size_t lo, hi;
+        flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
+        if (hi <= lo) continue;
+        (void)hipSetDevice(g->dev[r]);
+        hipError_t e = hipMemcpyAsync(out + lo, g->rk[r].shard, (hi - lo) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      flm::rt::stream_of(g->ctx[r]));
+        if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("shard D2H: ") + hipGetErrorString(e));
+    }
+    return flm_group_sync(g);
+}
+
+// Device-resident form: rank r's rows are already in its HBM (d_rows[r], n_rows[r] rows at
+// row_pitch), seeds/signs on every device.  Enqueues each rank's fused round and the exchange on
+// the ranks' streams (flm_group_ctx(g, r)'s stream) and returns; d_shards[r] (>= S words, S =
+// round_up(L, 1024*G)/G, on device r) receives rank r's slots [lo_r, hi_r) at offset 0.
+int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, size_t row_pitch, const int *n_rows,
+                                   const uint8_t *const *d_seeds, const int8_t *const *d_signs, int K, size_t L,
+                                   uint32_t *const *d_shards) {
+    if (!g) return gfail(nullptr, FLM_EINVAL, "group is NULL");
+    if (!n_rows || !d_shards || (K > 0 && (!d_seeds || !d_signs))) return gfail(g, FLM_EINVAL, "NULL argument");
+    if (L == 0) return 0;
+    const int G = g->n;
+    const uint64_t Lp = padded_len(L, G), S = Lp / G;
+    for (int r = 0; r < G; ++r)
+        if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
+    for (int r = 0; r < G; ++r) {
+        size_t lo, hi;
+        flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
+        flm_ctx *c = g->ctx[r];
+        int rc = flm_aggregate_unmask_dev(c, d_rows ? d_rows[r] : nullptr, row_pitch, n_rows[r],
+                                          K ? d_seeds[r] : nullptr, K ? d_signs[r] : nullptr, K, L, lo, hi, 0,
+                                          g->rk[r].partial, flm::rt::stream_of(c));
+        if (rc) return rank_error(g, r, rc);
+        if (hipEventRecord(g->rk[r].done, flm::rt::stream_of(c)) != hipSuccess) return gfail(g, FLM_EHIP, "event");
+    }
+    // the exchange writes the caller's shard buffers directly
+    return exchange(g, S, std::vector<uint32_t *>(d_shards, d_shards + G));
+}
+
+}  // extern "C"

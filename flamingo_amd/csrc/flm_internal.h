@@ -103,6 +103,13 @@ hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *
                              int groups, hipStream_t stream);
 hipError_t launch_flag_set(uint32_t *d_ws, hipStream_t stream);
 hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst, uint64_t n, hipStream_t stream);
+// dst[l] = sum_{g<G} d_parts[g][lo + l], l < n (G <= kMaxParts, all on the launching device).
+constexpr int kMaxParts = 16;
+struct PartPtrs {
+    const uint32_t *p[kMaxParts];
+};
+hipError_t launch_shard_sum(const uint32_t *const *d_parts, int G, uint64_t lo, uint64_t n, uint32_t *d_dst,
+                            hipStream_t stream);
 hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], uint64_t counter,
                                const uint8_t *d_in, uint8_t *d_out, size_t n, hipStream_t stream);
 
@@ -114,4 +121,20 @@ hipError_t launch_shamir_combine(const uint8_t *d_shares, const uint8_t *d_lambd
 hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T, int D, int negate,
                             uint8_t *d_points_out, uint8_t *d_digests_out, uint32_t *d_flags, hipStream_t stream);
 
+}  // namespace flm
+
+// Host-runtime hooks shared by flm_runtime.hip and flm_comm.hip (not exported in the header).
+struct flm_ctx;
+namespace flm {
+namespace rt {
+int set_error(flm_ctx *ctx, int code, const char *msg);
+int device_of(const flm_ctx *ctx);
+hipStream_t stream_of(const flm_ctx *ctx);
+void **comm_slot(flm_ctx *ctx);
+// Upload host rows and seeds and enqueue the fused round over mask window [mask_lo, mask_hi) into
+// d_out (L words) on the context's stream; returns without synchronising.
+int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,
+                     int K, size_t L, size_t mask_lo, size_t mask_hi, uint32_t *d_out);
+}  // namespace rt
+void comm_release(flm_ctx *ctx);  // flm_comm.hip: drop the context's communicator (flm_free)
 }  // namespace flm

@@ -734,6 +734,37 @@ __global__ __launch_bounds__(256) void add2_kernel(const uint32_t *__restrict__ 
     if (t < n) dst[t] = a[t] + b[t];
 }
 
+// Loopback exchange of a device group whose ranks share one GPU (flm_group with repeated
+// devices; tests and rehearsal only -- distinct GPUs use RCCL's reduce-scatter):
+// dst[l] = sum_g parts.p[g][lo + l] for l < n, mod 2^32.  HBM-bound, uint4 when aligned.
+__global__ __launch_bounds__(256) void shard_sum_kernel(PartPtrs parts, int G, uint64_t lo, uint64_t n,
+                                                        uint32_t *__restrict__ dst) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((lo & 3) == 0) {
+        const uint64_t quads = n / 4;
+        for (uint64_t q = t0; q < quads; q += stride) {
+            uint4 acc = make_uint4(0, 0, 0, 0);
+            for (int g = 0; g < G; ++g) {
+                const uint4 v = reinterpret_cast<const uint4 *>(parts.p[g] + lo)[q];
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+            reinterpret_cast<uint4 *>(dst)[q] = acc;
+        }
+        for (uint64_t t = 4 * quads + t0; t < n; t += stride) {
+            uint32_t a = 0;
+            for (int g = 0; g < G; ++g) a += parts.p[g][lo + t];
+            dst[t] = a;
+        }
+        return;
+    }
+    for (uint64_t t = t0; t < n; t += stride) {
+        uint32_t a = 0;
+        for (int g = 0; g < G; ++g) a += parts.p[g][lo + t];
+        dst[t] = a;
+    }
+}
+
 #undef FLM_QR
 #undef FLM_ROTL
 
@@ -850,6 +881,17 @@ hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst
     if (n == 0) return hipSuccess;
     const uint64_t g = std::min<uint64_t>(2048, (n / 4 + 255) / 256 + 1);
     hipLaunchKernelGGL(add2_kernel, dim3((unsigned)g), dim3(256), 0, stream, d_a, d_b, d_dst, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_shard_sum(const uint32_t *const *d_parts, int G, uint64_t lo, uint64_t n, uint32_t *d_dst,
+                            hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (G < 1 || G > kMaxParts) return hipErrorInvalidValue;
+    PartPtrs pp{};
+    for (int g = 0; g < G; ++g) pp.p[g] = d_parts[g];
+    const uint64_t grid = std::min<uint64_t>(2048, (n / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(shard_sum_kernel, dim3((unsigned)grid), dim3(256), 0, stream, pp, G, lo, n, d_dst);
     return hipGetLastError();
 }
 

@@ -111,6 +111,7 @@ struct flm_ctx {
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
+    void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
 
 namespace {
@@ -579,6 +580,29 @@ int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, cons
 
 }  // namespace
 
+namespace flm {
+namespace rt {
+int set_error(flm_ctx *ctx, int code, const char *msg) { return fail(ctx, code, "%s", msg); }
+int device_of(const flm_ctx *ctx) { return ctx->device; }
+hipStream_t stream_of(const flm_ctx *ctx) { return ctx->stream; }
+void **comm_slot(flm_ctx *ctx) { return &ctx->comm; }
+
+int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,
+                     int K, size_t L, size_t mask_lo, size_t mask_hi, uint32_t *d_out) {
+    if (N < 0 || K < 0) return fail(ctx, FLM_EINVAL, "negative N or K");
+    if ((N > 0 && !rows) || (K > 0 && (!seeds || !signs)) || !d_out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
+    if (int rc = check_range(ctx, L)) return rc;
+    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    const uint64_t pitch = round_up(L, 64);
+    if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
+    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    return flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, N, ctx->seeds.as<uint8_t>(),
+                                    ctx->signs.as<int8_t>(), K, L, mask_lo, mask_hi, 0, d_out, ctx->stream);
+}
+}  // namespace rt
+}  // namespace flm
+
 // ======================================================================= ABI
 extern "C" {
 
@@ -615,6 +639,7 @@ void flm_free(flm_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    flm::comm_release(ctx);
     for (auto &kv : ctx->plans) {
         kv.second->items.release();
         delete kv.second;

@@ -1,8 +1,7 @@
 """Multi-GPU server round: client-sharded rows, slot-sharded unmask, RCCL reduce-scatter.
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on
-ROCm).  Rank r of G holds the masked vectors of its own clients (the VECTOR
-bodies it ingested over its own PCIe link) and owns slot shard
+One process per GPU.  Rank r of G holds the masked vectors of its own clients
+(the VECTOR bodies it ingested over its own PCIe link) and owns slot shard
 [r*S, (r+1)*S) of the output, S = Lp / G with Lp = L rounded up to 1024*G:
 
   partial_r[l] = sum_{i in clients(r)} y_i[l]                    l in [0, L)
@@ -15,6 +14,15 @@ is associative and commutative mod 2^32, so every ring order gives the same
 bits.  Each rank regenerates all K masks but only over its own slots, which
 splits the VALU-bound ChaCha work G ways; the row sum (HBM-bound) is split by
 clients.  The only collective is one reduce-scatter of Lp*4 bytes per round.
+
+The collective runs through the library's own RCCL communicator
+(flm_comm_init_rank / flm_reduce_scatter_dev: ncclReduceScatter with ncclUint32,
+enqueued on the same HIP stream as the kernel that wrote the partial) when one
+is attached -- ``init_rccl`` does that over an existing torch.distributed group.
+Without one (gloo tests on CPU, or several ranks sharing one GPU, where RCCL
+refuses duplicate devices) the same exchange goes through torch.distributed.
+The shard geometry is the library's (flm_shard_bounds / flm_client_bounds), so
+the single-process DeviceGroup and these per-process ranks cut the round alike.
 """
 from __future__ import annotations
 
@@ -30,7 +38,7 @@ def padded_length(L: int, world: int) -> int:
 
 
 def shard_bounds(L: int, world: int, rank: int):
-    """[lo, hi) of output slots owned by `rank` (hi clipped to L; may be empty)."""
+    """[lo, hi) of output slots owned by `rank` (hi clipped to L; may be empty).  Same as flm_shard_bounds."""
     S = padded_length(L, world) // world
     lo = min(rank * S, L)
     hi = min((rank + 1) * S, L)
@@ -38,32 +46,63 @@ def shard_bounds(L: int, world: int, rank: int):
 
 
 def client_bounds(N: int, world: int, rank: int):
-    """Contiguous block of clients ingested by `rank`."""
+    """Contiguous block of clients ingested by `rank` (flm_client_bounds)."""
     return N * rank // world, N * (rank + 1) // world
+
+
+def init_rccl(engine, group=None):
+    """Attach an RCCL communicator over `group`'s ranks to `engine` (collective).
+
+    Rank 0 makes the unique id (flm_comm_unique_id) and torch.distributed broadcasts it;
+    every rank then joins with flm_comm_init_rank.  Returns (world, rank)."""
+    from .engine import comm_unique_id
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    box = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    engine.comm_init(world, rank, box[0])
+    return world, rank
+
+
+def _torch_stream(stream):
+    if stream is None or isinstance(stream, torch.cuda.Stream):
+        return stream
+    return torch.cuda.ExternalStream(int(stream))
 
 
 class ShardedRound:
     """Runs one rank's share of a round on its GPU and reduce-scatters the partials.
 
-    With buffers=2, launch() leaves the reduce-scatter in flight (async_op) and the
-    next round's kernel writes the other partial buffer, so round k's collective over
-    xGMI runs under round k+1's kernel; a buffer is reused only after the collective
-    that read it has completed (a stream-side wait, the host never blocks)."""
+    With buffers=2, launch() leaves the reduce-scatter in flight and the next round's
+    kernel writes the other partial buffer, so round k's collective over xGMI runs under
+    round k+1's kernel; a buffer is reused only after the collective that read it has
+    completed (a stream-side wait, the host never blocks).  On the RCCL path the
+    collective runs on a comm stream of its own, ordered after the kernel by an event."""
 
-    def __init__(self, engine, L: int, group=None, device=None, buffers: int = 1):
+    def __init__(self, engine, L: int, group=None, device=None, buffers: int = 1, comm: str | None = None):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.L = L
         self.Lp = padded_length(L, self.world)
+        self.S = self.Lp // self.world
         self.lo, self.hi = shard_bounds(L, self.world, self.rank)
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if buffers not in (1, 2):
             raise ValueError("buffers must be 1 or 2")
+        if comm is None:
+            comm = "rccl" if (engine is not None and self.world > 1 and engine.comm_size() == (self.world, self.rank)) \
+                else "torch"
+        if comm not in ("rccl", "torch"):
+            raise ValueError("comm must be 'rccl' or 'torch'")
+        if comm == "rccl" and engine.comm_size() != (self.world, self.rank):
+            raise RuntimeError("comm='rccl' needs init_rccl(engine, group) first")
+        self.comm = comm
         self._partials = [torch.zeros(self.Lp, dtype=torch.int32, device=dev) for _ in range(buffers)]
-        self._outs = [torch.empty(self.Lp // self.world, dtype=torch.int32, device=dev) for _ in range(buffers)]
-        self._pending = [None] * buffers
+        self._outs = [torch.empty(self.S, dtype=torch.int32, device=dev) for _ in range(buffers)]
+        self._pending = [None] * buffers          # torch Work (torch path) or comm-done Event (rccl path)
+        self._comm_stream = torch.cuda.Stream(device=dev) if (comm == "rccl" and buffers == 2) else None
         self._k = 0
         self.partial, self.out = self._partials[0], self._outs[0]
 
@@ -76,37 +115,56 @@ class ShardedRound:
         self.engine.aggregate_dev(d_rows, self.K, self.partial, L=self.L, mask_lo=self.lo, mask_hi=self.hi,
                                   stream=stream)
 
-    def exchange(self):
-        if self.world == 1:
-            return self.partial[: self.L]
+    def _torch_exchange(self, async_op: bool = False):
         if self.partial.is_cuda and dist.get_backend(self.group) == "gloo":
             # test path only (several ranks sharing one GPU, where RCCL refuses duplicate
             # devices): the same reduce-scatter on host copies
             cpu_out = torch.empty(self.out.shape, dtype=self.out.dtype)
             dist.reduce_scatter_tensor(cpu_out, self.partial.cpu(), op=dist.ReduceOp.SUM, group=self.group)
             self.out.copy_(cpu_out)
+            return None
+        return dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=async_op)
+
+    def exchange(self, stream=None):
+        """The reduce-scatter of the current partial, ordered after the work on `stream`."""
+        if self.world == 1:
+            return self.partial[: self.L]
+        if self.comm == "rccl":
+            self.engine.reduce_scatter_dev(self.partial, self.out, self.S, stream=stream)
         else:
-            dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM, group=self.group)
+            st = _torch_stream(stream)
+            if st is not None and self.partial.is_cuda:
+                with torch.cuda.stream(st):           # torch's collective orders against the CURRENT stream
+                    self._torch_exchange()
+            else:
+                self._torch_exchange()
         return self.out[: self.hi - self.lo]
 
     def step(self, d_rows, d_seeds, d_signs, stream=None):
         self.prepare_seeds(d_seeds, d_signs, stream)
         self.compute(d_rows, stream)
-        return self.exchange()
+        return self.exchange(stream)
 
     def _async_ok(self):
         # RCCL (or gloo on host tensors) can leave the collective in flight; the gloo path
         # over a shared GPU (tests only) goes through host copies and stays synchronous
-        return self.world > 1 and not (self.partial.is_cuda and dist.get_backend(self.group) == "gloo")
+        if self.world == 1:
+            return False
+        if self.comm == "rccl":
+            return self._comm_stream is not None
+        return not (self.partial.is_cuda and dist.get_backend(self.group) == "gloo")
 
     def launch(self, d_rows, d_seeds, d_signs, stream=None) -> int:
         """Enqueue one round; returns its buffer index for result()."""
         b = self._k % len(self._partials)
+        st = _torch_stream(stream)
         if self._pending[b] is not None:
-            # the collective that last read this buffer: Work.wait() makes the CURRENT
-            # stream wait, so make that the stream the kernel is enqueued on
-            if stream is not None and isinstance(stream, torch.cuda.Stream):
-                with torch.cuda.stream(stream):
+            # the collective that last read this buffer must finish before the kernel rewrites it
+            if self.comm == "rccl":
+                (st or torch.cuda.current_stream()).wait_event(self._pending[b])
+            elif st is not None and self.partial.is_cuda:
+                with torch.cuda.stream(st):            # Work.wait() makes the CURRENT stream wait
                     self._pending[b].wait()
             else:
                 self._pending[b].wait()
@@ -114,11 +172,21 @@ class ShardedRound:
         self.partial, self.out = self._partials[b], self._outs[b]
         self.prepare_seeds(d_seeds, d_signs, stream)
         self.compute(d_rows, stream)
-        if self._async_ok():
-            self._pending[b] = dist.reduce_scatter_tensor(self.out, self.partial, op=dist.ReduceOp.SUM,
-                                                          group=self.group, async_op=True)
+        if not self._async_ok():
+            self.exchange(stream)
+        elif self.comm == "rccl":
+            ready = torch.cuda.Event()
+            ready.record(st or torch.cuda.current_stream())
+            self._comm_stream.wait_event(ready)
+            self.engine.reduce_scatter_dev(self.partial, self.out, self.S, stream=self._comm_stream)
+            done = torch.cuda.Event()
+            done.record(self._comm_stream)
+            self._pending[b] = done
+        elif st is not None and self.partial.is_cuda:
+            with torch.cuda.stream(st):
+                self._pending[b] = self._torch_exchange(async_op=True)
         else:
-            self.exchange()
+            self._pending[b] = self._torch_exchange(async_op=True)
         self._k += 1
         return b
 
@@ -126,7 +194,10 @@ class ShardedRound:
         """This rank's shard of round `b` (default: the last launched), after its collective."""
         b = (self._k - 1) % len(self._partials) if b is None else b
         if self._pending[b] is not None:
-            self._pending[b].wait()
+            if self.comm == "rccl":
+                torch.cuda.current_stream().wait_event(self._pending[b])
+            else:
+                self._pending[b].wait()
             self._pending[b] = None
         if self.world == 1:
             return self._partials[b][: self.L]

@@ -54,9 +54,13 @@ def _signs_array(signs, K: int) -> np.ndarray:
 class MaskEngine:
     """One GPU's mask-and-aggregate engine (a flm_ctx)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, _ctx=None):
         self.lib = _lib.load()
         self.device = device
+        self._owned = _ctx is None
+        if _ctx is not None:                 # a context owned by a DeviceGroup
+            self.ctx = ctypes.c_void_p(_ctx)
+            return
         ctx = ctypes.c_void_p()
         rc = self.lib.flm_init(ctypes.byref(ctx), device)
         if rc != 0:
@@ -65,6 +69,9 @@ class MaskEngine:
 
     # ------------------------------------------------------------ plumbing
     def close(self):
+        if not getattr(self, "_owned", True):
+            self.ctx = None
+            return
         if getattr(self, "ctx", None) is not None and self.ctx.value:
             for st in self.__dict__.pop("_cu_streams", {}).values():
                 st.synchronize()
@@ -122,6 +129,36 @@ class MaskEngine:
                                                         ctypes.byref(h)), "flm_stream_create_cu_mask")
         cache[cus] = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", self.device))
         return cache[cus]
+
+    # ----------------------------------------------- RCCL (one process per GPU)
+    def comm_init(self, n_ranks: int, rank: int, unique_id: bytes):
+        """Attach an RCCL communicator (flm_comm_init_rank; collective over all ranks)."""
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        self._check(self.lib.flm_comm_init_rank(self.ctx, int(n_ranks), int(rank), uid), "flm_comm_init_rank")
+
+    def comm_size(self):
+        """(n_ranks, rank) of the attached communicator, (1, 0) without one."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        self.lib.flm_comm_size(self.ctx, ctypes.byref(n), ctypes.byref(r))
+        return n.value, r.value
+
+    def reduce_scatter_dev(self, send, recv, recv_words: int | None = None, stream=None):
+        """recv[:recv_words] = this rank's slice of sum_ranks(send) as uint32 (ncclUint32, ncclSum)."""
+        n = int(recv.numel() if recv_words is None else recv_words)
+        if send.numel() < n * self.comm_size()[0] or recv.numel() < n or send.element_size() != 4:
+            raise RuntimeError("reduce_scatter_dev: send must hold n_ranks * recv_words 32-bit words")
+        self._check(self.lib.flm_reduce_scatter_dev(self.ctx, send.data_ptr(), recv.data_ptr(), n,
+                                                    self._stream_handle(stream)), "flm_reduce_scatter_dev")
+        return recv
+
+    def all_gather_dev(self, send, recv, stream=None):
+        """recv = concat over ranks of send's bytes (ncclAllGather, ncclUint8)."""
+        nb = send.numel() * send.element_size()
+        if recv.numel() * recv.element_size() < nb * self.comm_size()[0]:
+            raise RuntimeError("all_gather_dev: recv too small")
+        self._check(self.lib.flm_all_gather_dev(self.ctx, send.data_ptr(), recv.data_ptr(), nb,
+                                                self._stream_handle(stream)), "flm_all_gather_dev")
+        return recv
 
     # -------------------------------------------------------- host arrays
     def aggregate_unmask(self, vectors, seeds, signs, L: int | None = None) -> np.ndarray:
@@ -497,3 +534,121 @@ class PinnedArena:
         if self.ptr:
             self.lib.flm_host_free(self.ptr)
             self.ptr = None
+
+
+# ------------------------------------------------------------------ multi-GPU
+def comm_unique_id() -> bytes:
+    """A fresh 128-byte RCCL unique id (flm_comm_unique_id), for rank 0 to broadcast."""
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * 128)()
+    rc = lib.flm_comm_unique_id(buf)
+    if rc != 0:
+        raise RuntimeError(f"flm_comm_unique_id: {lib.flm_last_error(None).decode()}")
+    return bytes(buf)
+
+
+def shard_bounds(L: int, n_ranks: int, rank: int):
+    """(lo, hi, S): rank's output slots [lo, hi) and the shard length S (flm_shard_bounds)."""
+    lib = _lib.load()
+    lo, hi, S = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    if lib.flm_shard_bounds(int(L), int(n_ranks), int(rank), ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(S)):
+        raise RuntimeError("flm_shard_bounds: bad arguments")
+    return lo.value, hi.value, S.value
+
+
+def client_bounds(N: int, n_ranks: int, rank: int):
+    """[c0, c1): the clients rank ingests (flm_client_bounds)."""
+    lib = _lib.load()
+    c0, c1 = ctypes.c_int(), ctypes.c_int()
+    if lib.flm_client_bounds(int(N), int(n_ranks), int(rank), ctypes.byref(c0), ctypes.byref(c1)):
+        raise RuntimeError("flm_client_bounds: bad arguments")
+    return c0.value, c1.value
+
+
+class DeviceGroup:
+    """All GPUs of the node from ONE process (flm_group): the drop-in server's multi-GPU form.
+
+    The reference server is a single-threaded DES process (Kernel.py:190-271); a group gives
+    its report/reconstruction steps every device: client-sharded upload and row sum,
+    slot-sharded unmask, one RCCL reduce-scatter (ncclUint32), shards back to the host.
+    devices: distinct ids (RCCL clique) or one id repeated (loopback ranks on one GPU)."""
+
+    def __init__(self, devices):
+        self.lib = _lib.load()
+        if isinstance(devices, int):
+            devices = list(range(devices))
+        devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(devices))(*devices)
+        g = ctypes.c_void_p()
+        rc = self.lib.flm_group_init(ctypes.byref(g), len(devices), arr)
+        if rc != 0:
+            raise RuntimeError(f"flm_group_init({devices}): {self.lib.flm_group_last_error(None).decode()}")
+        self.g = g
+        self.devices = devices
+        self.n = len(devices)
+        self.loopback = bool(self.lib.flm_group_is_loopback(g))
+        self.engines = [MaskEngine(d, _ctx=self.lib.flm_group_ctx(g, r)) for r, d in enumerate(devices)]
+
+    def close(self):
+        if getattr(self, "g", None) is not None and self.g.value:
+            for e in self.engines:
+                e.close()
+            self.lib.flm_group_free(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.flm_group_last_error(self.g).decode()} (code {rc})")
+
+    def sync(self):
+        self._check(self.lib.flm_group_sync(self.g), "flm_group_sync")
+
+    def aggregate_unmask(self, vectors, seeds, signs, L: int | None = None) -> np.ndarray:
+        """MaskEngine.aggregate_unmask over every device of the group (host rows in, host out)."""
+        if isinstance(vectors, np.ndarray) and vectors.ndim == 2:
+            rows = [np.ascontiguousarray(vectors[i], dtype=np.uint32) for i in range(vectors.shape[0])]
+        else:
+            rows = [np.ascontiguousarray(v, dtype=np.uint32) for v in vectors]
+        if L is None:
+            if not rows:
+                raise RuntimeError("L is required when there are no vectors")
+            L = rows[0].shape[0]
+        for v in rows:
+            if v.shape[0] != L:
+                raise RuntimeError("Client sends vector of incorrect length.")  # SA_ServiceAgent.py:348-349
+        seeds = _seeds_array(seeds)
+        signs = _signs_array(signs, seeds.shape[0])
+        out = np.empty(L, dtype=np.uint32)
+        ptrs = (_lib._u32p * max(1, len(rows)))(*[p_u32(v) for v in rows])
+        self._check(self.lib.flm_group_aggregate_unmask(self.g, ptrs, len(rows), p_u8(seeds), p_i8(signs),
+                                                        seeds.shape[0], L, p_u32(out)),
+                    "flm_group_aggregate_unmask")
+        return out
+
+    def aggregate_unmask_dev(self, rows, seeds, signs, shards, L: int):
+        """rows/seeds/signs/shards: per-rank CUDA tensors on the ranks' devices (rows (N_r, pitch) with one
+        common pitch; shards >= S words).  Enqueued on the ranks' streams; call sync() before reading."""
+        n = self.n
+        pitch = max((r.shape[1] for r in rows if r is not None and r.shape[0]), default=0)
+        K = seeds[0].shape[0] if seeds and seeds[0] is not None else 0
+        vp = ctypes.c_void_p
+        d_rows = (vp * n)(*[r.data_ptr() if r is not None and r.shape[0] else 0 for r in rows])
+        n_rows = (ctypes.c_int * n)(*[int(r.shape[0]) if r is not None else 0 for r in rows])
+        d_seeds = (vp * n)(*[s.data_ptr() if K else 0 for s in seeds])
+        d_signs = (vp * n)(*[s.data_ptr() if K else 0 for s in signs])
+        d_shards = (vp * n)(*[s.data_ptr() for s in shards])
+        self._check(self.lib.flm_group_aggregate_unmask_dev(self.g, d_rows, pitch, n_rows, d_seeds, d_signs, K, L,
+                                                            d_shards), "flm_group_aggregate_unmask_dev")
+        return shards

@@ -253,6 +253,61 @@ int flm_cu_count(flm_ctx *ctx, int *n_cus);
 int flm_stream_create_cu_mask(flm_ctx *ctx, const uint32_t *mask, int n_words, void **stream_out);
 int flm_stream_destroy(flm_ctx *ctx, void *stream);
 
+/* ------------------------------------------------ multi-GPU (RCCL over xGMI) */
+
+/* The round shards two ways over G GPUs: rank r ingests clients
+ * [N*r/G, N*(r+1)/G) and sums them over all L slots, regenerates every seed's
+ * mask over its own slot shard [lo_r, hi_r) only, and ONE reduce-scatter of the
+ * partial vectors (ncclUint32, ncclSum -- mod 2^32, so every ring order gives
+ * the same bits) returns rank r the slots [lo_r, hi_r) of the reference's
+ * final_sum = vec_sum_partial + cancel_vec + mi_vec (SA_ServiceAgent.py:346-350,
+ * 529-605).  Shards are S = round_up(L, 1024*G) / G slots (the partial vectors
+ * are S*G long); trailing ranks may own an empty shard. */
+int flm_shard_bounds(size_t L, int n_ranks, int rank, size_t *lo, size_t *hi, size_t *shard_words);
+int flm_client_bounds(int N, int n_ranks, int rank, int *c0, int *c1);
+
+/* One process per GPU: rank 0 makes a 128-byte RCCL unique id, every rank
+ * passes it to flm_comm_init_rank (collective: all ranks must call it), and the
+ * context then owns the communicator (released by flm_free).
+ * flm_reduce_scatter_dev: d_recv[0..recv_words) = rank's slice of the elementwise
+ * uint32 sum over ranks of d_send[0..recv_words*n_ranks).  flm_all_gather_dev:
+ * byte all-gather (d_recv = n_ranks * send_bytes), e.g. recovered pair seeds.
+ * stream NULL = the context's stream.  flm_comm_size returns 1 when no
+ * communicator is attached (then *n_ranks = 1, *rank = 0). */
+int flm_comm_unique_id(uint8_t id_out[128]);
+int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128]);
+int flm_comm_size(flm_ctx *ctx, int *n_ranks, int *rank);
+int flm_reduce_scatter_dev(flm_ctx *ctx, const uint32_t *d_send, uint32_t *d_recv, size_t recv_words, void *stream);
+int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t send_bytes, void *stream);
+
+/* One process, G GPUs -- the drop-in server's form: the reference server is a
+ * single-threaded DES process (Kernel.py:190-271), so the group owns one
+ * context per device and an RCCL clique (ncclCommInitAll).  devices: G device
+ * ids, all distinct (RCCL) or all equal (loopback: the ranks share one GPU and
+ * exchange through a device kernel instead of RCCL -- tests and rehearsal on a
+ * one-GPU box); NULL = 0..G-1.  G <= 16.
+ * flm_group_aggregate_unmask: flm_aggregate_unmask over every device: host
+ * rows in (one host thread per device uploads that device's clients), out (L
+ * words, host) back; synchronous.
+ * flm_group_aggregate_unmask_dev: rows already resident (d_rows[r]: n_rows[r]
+ * rows at row_pitch on device r; d_seeds[r]/d_signs[r] on device r); enqueues
+ * every rank's round and the exchange on the ranks' context streams and
+ * returns; d_shards[r] (>= S words on device r) receives slots [lo_r, hi_r).
+ * flm_group_sync waits for every rank's stream. */
+typedef struct flm_group flm_group;
+int flm_group_init(flm_group **out, int n, const int *devices);
+void flm_group_free(flm_group *g);
+const char *flm_group_last_error(const flm_group *g);
+int flm_group_size(const flm_group *g);
+int flm_group_is_loopback(const flm_group *g);
+flm_ctx *flm_group_ctx(flm_group *g, int rank);
+int flm_group_sync(flm_group *g);
+int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N, const uint8_t *seeds,
+                               const int8_t *signs, int K, size_t L, uint32_t *out);
+int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, size_t row_pitch, const int *n_rows,
+                                   const uint8_t *const *d_seeds, const int8_t *const *d_signs, int K, size_t L,
+                                   uint32_t *const *d_shards);
+
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */
 void *flm_host_alloc(size_t bytes);

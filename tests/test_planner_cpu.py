@@ -121,3 +121,28 @@ def test_pick_cus_balances_xcds():
         assert per_xcd.min() == per_xcd.max() == k // 8
     st = pick_cus(256, 24, "stride")
     assert len(st) == 24 and max(st) < 256
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 7, 8, 16])
+def test_shard_and_client_bounds_partition_the_round(G):
+    """flm_shard_bounds / flm_client_bounds (the library's multi-GPU geometry, host-only): the
+    shards tile [0, L) in order with 16-slot-aligned starts, each S = round_up(L, 1024 G)/G long
+    at most; clients tile [0, N); and distributed.py's Python view agrees."""
+    from flamingo_amd import distributed as D
+    from flamingo_amd.engine import client_bounds, shard_bounds
+    for L in (1, 15, 1000, 16000, 16384, 70000, 1 << 18, (1 << 20) + 48):
+        prev = 0
+        for r in range(G):
+            lo, hi, S = shard_bounds(L, G, r)
+            assert (lo, hi) == D.shard_bounds(L, G, r)
+            assert S * G == D.padded_length(L, G) and S % 1024 == 0
+            assert lo == prev and lo <= hi and hi - lo <= S and (lo % 16 == 0 or lo == hi == L)
+            prev = hi
+        assert prev == L
+    for N in (0, 1, 5, 128, 1024, 4096):
+        prev = 0
+        for r in range(G):
+            c0, c1 = client_bounds(N, G, r)
+            assert (c0, c1) == D.client_bounds(N, G, r) and c0 == prev and c0 <= c1
+            prev = c1
+        assert prev == N

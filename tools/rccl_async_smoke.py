@@ -1,6 +1,8 @@
 """One-rank RCCL run of ShardedRound's pipelined path (buffers=2, async reduce-scatter, stream-side
 waits) on a one-GPU box: with world_size 1 the collective is a copy, but the Work/stream handling
-is exactly the multi-GPU code.  Checks every round's shard against the synchronous round."""
+is exactly the multi-GPU code.  Checks every round's shard against the synchronous round, for both
+exchanges: torch.distributed's reduce-scatter and the library's own communicator
+(init_rccl -> flm_comm_init_rank, flm_reduce_scatter_dev with ncclUint32 on a comm stream)."""
 import os
 import sys
 
@@ -9,13 +11,14 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flamingo_amd import MaskEngine  # noqa: E402
-from flamingo_amd.distributed import ShardedRound  # noqa: E402
+from flamingo_amd.distributed import ShardedRound, init_rccl  # noqa: E402
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29561")
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 eng = MaskEngine(0)
+print("library communicator:", init_rccl(eng), flush=True)
 N, K, L = 64, 48, 1 << 16
 g = torch.Generator(device="cuda")
 g.manual_seed(3)
@@ -30,20 +33,21 @@ for r in rows:
     torch.cuda.synchronize()
     want.append(res.clone())
 torch.cuda.synchronize()
-pipe = ShardedRound(eng, L, buffers=2)
-pipe._async_ok = lambda: True          # world 1: force the RCCL async path
 ok = True
-with torch.cuda.stream(stream):
-    for rep in range(4):
-        bufs = [pipe.launch(r, seeds, signs, stream) for r in rows]
-        torch.cuda.synchronize()
-        got = [pipe._outs[b][:L] for b in bufs[-2:]]
-        parts = [pipe._partials[b][:L] for b in bufs[-2:]]
-        for i, (o, p_, w) in enumerate(zip(got, parts, want[1:])):
-            e = bool(torch.equal(o, w))
-            print(f"rep {rep} round {i + 1}: out==want {e}  partial==want {bool(torch.equal(p_, w))} "
-                  f"mismatches {int((o != w).sum())}", flush=True)
-            ok &= e
+for comm in ("torch", "rccl"):
+    pipe = ShardedRound(eng, L, buffers=2, comm=comm)
+    pipe._async_ok = lambda: True          # world 1: force the async path
+    with torch.cuda.stream(stream):
+        for rep in range(4):
+            bufs = [pipe.launch(r, seeds, signs, stream) for r in rows]
+            torch.cuda.synchronize()
+            got = [pipe._outs[b][:L] for b in bufs[-2:]]
+            parts = [pipe._partials[b][:L] for b in bufs[-2:]]
+            for i, (o, p_, w) in enumerate(zip(got, parts, want[1:])):
+                e = bool(torch.equal(o, w))
+                print(f"{comm} rep {rep} round {i + 1}: out==want {e}  partial==want {bool(torch.equal(p_, w))} "
+                      f"mismatches {int((o != w).sum())}", flush=True)
+                ok &= e
 print(f"rccl async pipelined rounds ok={ok}", flush=True)
 dist.destroy_process_group()
 eng.close()
