@@ -5,13 +5,14 @@ Contract (see README/DESIGN.md): ``python bench.py --gpus N --steps K --warmup W
 prints ONE JSON line on rank 0.  For N > 1 it is launched by torch.distributed.run
 (one process per GPU, RCCL over xGMI).
 
-Workload (BASELINE.json configs[3], "c4"): every GPU ingests 1024 clients'
-masked vectors of L = 2^20 uint32 slots; the round has N_total = 1024 * G
-clients, no dropouts, so K = N_total self-mask seeds are regenerated
-(SA_ServiceAgent.py:529-536) and the output is sum(y_i) - sum PRG(m_i) = |U|
-in every slot (checked after timing).  Per-GPU work is fixed as G grows
-(weak scaling): rows 1024 x L per GPU, masks K x L/G per GPU.  --total-clients N runs
-BASELINE c4 literally instead (strong scaling: N clients in all, N/G rows per GPU).
+Workload (BASELINE.json configs[3], "c4"): N = 1024 clients' masked vectors of
+L = 2^20 uint32 slots in all, split over the G ranks (strong scaling, the config
+literally: "n=1024 clients, L=2^20, vector slots sharded across 8 GPUs"); no
+dropouts, so K = 1024 self-mask seeds are regenerated (SA_ServiceAgent.py:529-536)
+and the output is sum(y_i) - sum PRG(m_i) = |U| in every slot (checked after
+timing).  Rank r ingests clients [N r/G, N (r+1)/G) and regenerates the K masks over
+its slot shard only.  --weak runs --clients-per-gpu clients on EVERY rank instead
+(N = 1024 G; per-GPU work fixed), reported as "scaling": "weak".
 
 A step = one round on device-resident inputs: seed-schedule launch +
 row-sum/unmask launch (+ RCCL reduce-scatter of the L-slot partial for G > 1).
@@ -49,10 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--total-clients", type=int, default=1024,
+                    help="clients in all, split over the ranks (BASELINE c4: 1024 over 1-8 GPUs, strong scaling)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling instead: --clients-per-gpu clients on every rank (N = clients-per-gpu * G)")
     ap.add_argument("--clients-per-gpu", type=int, default=1024)
-    ap.add_argument("--total-clients", type=int, default=0,
-                    help="strong scaling: this many clients in all, split over the ranks (BASELINE c4 literally: "
-                         "1024 over 8 GPUs); default 0 = weak scaling, --clients-per-gpu on every rank")
     ap.add_argument("--log2-L", type=int, default=20)
     ap.add_argument("--dropout", type=float, default=0.0, help="fraction of clients offline (c5: 0.01)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -90,11 +92,13 @@ def main():
 
     from flamingo_amd import MaskEngine
     from flamingo_amd import params as P
-    from flamingo_amd.distributed import ShardedRound, client_bounds
+    from flamingo_amd.distributed import ShardedRound, client_bounds, init_rccl
 
     eng = MaskEngine(torch.cuda.current_device())
+    if G > 1 and args.dist_backend == "nccl":
+        init_rccl(eng)          # the library's own RCCL communicator: ncclUint32 reduce-scatter on our stream
     L = 1 << args.log2_L
-    strong = args.total_clients > 0
+    strong = not args.weak
     N = args.total_clients if strong else args.clients_per_gpu * G
     Ng = N // G if strong else args.clients_per_gpu
     cfg = f"c4-n{N}-L{L}"
@@ -212,7 +216,7 @@ def main():
                    "clients": N, "clients_per_gpu": Ng, "online": int(len(online)), "L": L, "seeds_K": int(K),
                    "dropout_pairs_D": int(D),
                    "parallelism": f"client-shard{G}+slot-shard{G}" + (
-                       f"+{'rccl' if args.dist_backend == 'nccl' else args.dist_backend}-reduce-scatter-overlapped"
+                       f"+{'rccl-uint32' if rnd.comm == 'rccl' else args.dist_backend}-reduce-scatter-overlapped"
                        if G > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
@@ -228,6 +232,11 @@ def main():
                           "ceiling_source": "profiles/r01_issue_probe.log (QR8 lockstep: 3.52 cycles per instruction)"},
     }
 
+    if not args.profile:
+        ceil = mask_only_ceiling(eng, torch, d_seeds, d_signs, L, rnd.lo, rnd.hi, stream)
+        res["roofline_valu"]["same_run_ceiling"] = ceil
+        res["roofline_valu"]["frac_of_same_run_ceiling"] = round(
+            words / (kms * 1e-3) / 1e9 / ceil["mask_gwords_per_s"], 4)
     tr = committed_traffic(rows_rank, L, int(K))
     if tr is not None:
         res["roofline"]["traffic"] = tr["bytes"]
@@ -251,6 +260,9 @@ def main():
             res["with_copy"] = with_copy(eng, torch, rows_on, sseeds, ssigns, L, len(online))
         if not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(rows_on, sseeds, ssigns, L, out)
+    if G > 1 and not args.profile and not args.no_configs:
+        res["other_configs"] = {"c5": measure_c5_sharded(eng, torch, dist, P, G, rank,
+                                                         backend=args.dist_backend)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if G > 1:
@@ -482,6 +494,93 @@ def measure_recovery(eng, torch, D, M, T, steps=10):
                              "lagrange_ms": round(cpu_lagrange_ms, 1)}}
 
 
+def mask_only_ceiling(eng, torch, d_seeds, d_signs, L, lo, hi, stream, reps=10):
+    """The ChaCha ceiling measured in the same run: the timed round's own K seeds over its own
+    slot window, no rows (a mask-only items_kernel launch), right after the timed loop so the
+    clock is the one the round ran at.  Median of `reps` launches."""
+    K = d_seeds.shape[0]
+    out = torch.empty(L, dtype=torch.int32, device=d_seeds.device)
+    eng.seed_table_dev(d_seeds, d_signs, stream=stream)
+    for _ in range(3):
+        eng.aggregate_dev(None, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(stream)
+    for i in range(reps):
+        eng.aggregate_dev(None, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))
+    words = float(K) * (hi - lo)
+    return {"what": "mask-only launch of the same K seeds over the same slot window (no rows), same run",
+            "kernel_ms": round(ms, 4), "mask_gwords_per_s": round(words / (ms * 1e-3) / 1e9, 1)}
+
+
+def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, steps=5):
+    """BASELINE c5 on G GPUs (n=4096, L=2^20, 1 % dropouts, 10 iterations): every rank runs
+    flamingo_amd.dist_recon.ShardedReconstruction on its share -- its online clients' rows, all
+    m_i (Shamir), its chunk of the dropout pairs (EC combine on a side stream), one all-gather of
+    the pair keys, the pair masks over its slot shard, one reduce-scatter.  Wall time per round,
+    barrier-bracketed, max over ranks; every rank checks its shard == |U|."""
+    from flamingo_amd.dist_recon import ShardedReconstruction, pair_chunk
+    from flamingo_amd.distributed import client_bounds
+    from flamingo_amd.synthetic import recovery_round
+    dev = torch.device("cuda", torch.cuda.current_device())
+    N, L, T = 4096, 1 << 20, 20
+    m = np.frombuffer(b"".join(P.bench_seed("c5", i) for i in range(N)), np.uint8).reshape(N, 32)
+    stream = torch.cuda.current_stream()
+    rec = ShardedReconstruction(eng, L, comm="rccl" if backend == "nccl" else "torch")
+    out = torch.empty(rec.S, dtype=torch.int32, device=dev)
+    per_round, oks, Ds = [], True, []
+    cache = {}
+    coll = dev if backend == "nccl" else torch.device("cpu")
+    for it in range(1, rounds + 1):
+        nbrs = P.neighbor_graph(b"\x00" * 32, it, N, 1, encrypt=eng.chacha20_encrypt)
+        off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, int(round(0.01 * N)), replace=False))
+        on = np.setdiff1d(np.arange(N), off)
+        R = recovery_round(eng, m, nbrs, on, off, T=T, committee=60, seed=it, point_cache=cache)
+        c0, c1 = client_bounds(len(on), G, rank)
+        ids = on[c0:c1]
+        seg = R["seg"]
+        st, en = seg[ids], seg[ids + 1]
+        sub_seeds = np.concatenate([R["client_seeds"][a:b] for a, b in zip(st, en)])
+        sub_signs = np.concatenate([R["client_signs"][a:b] for a, b in zip(st, en)])
+        sub_seg = np.concatenate([[0], np.cumsum(en - st)]).astype(np.int64)
+        rows = torch.empty((len(ids), L), dtype=torch.int32, device=dev)
+        eng.client_mask_dev(sub_seg, torch.from_numpy(sub_seeds).to(dev), sub_signs, rows, L, stream=stream)
+        D = R["D"]
+        a, b, _ = pair_chunk(D, G, rank)
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        args = (rows, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]), t(R["pair_shares"][:, a:b]),
+                t(R["pair_signs"]), D, out)
+        for _ in range(2):
+            rec.run(*args, stream=stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rec.run(*args, stream=stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        per_round.append(float(el.item()) / steps * 1e3)
+        oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
+        Ds.append(D)
+        del rows
+    okt = torch.tensor([1 if oks else 0], device=coll)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    ms = float(np.mean(per_round))
+    return {"clients": N, "L": L, "dropout": 0.01, "iterations": rounds, "decryptors_T": T,
+            "dropout_pairs_D_mean": float(np.mean(Ds)),
+            "server_reconstruction_ms": round(ms, 4),
+            "GB/s": round((4.0 * (N - round(0.01 * N)) * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
+            "correct": bool(okt.item()),
+            "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
+                        "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "
+                        "shard; reduce-scatter (library RCCL communicator, ncclUint32)"}
+
+
 def committed_traffic(rows, L, K):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/*_profile_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when the
@@ -556,6 +655,34 @@ def with_copy(eng, torch, rows, seeds, signs, L, n_online):
                     "hipMemcpyAsync over 4 copy streams, + D2H of out"}
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def host_threads():
+    """(threads, quota): every core this job may use -- nproc, capped by the cgroup CPU quota
+    (cpu.max) when one is set -- and that quota in cores (None when unlimited)."""
+    n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    if hasattr(os, "sched_getaffinity"):
+        n = min(n, len(os.sched_getaffinity(0)))
+    return (max(1, min(n, int(quota))) if quota else n), quota
+
+
 def cpu_baseline(rows, seeds, signs, L, gpu_out):
     """CPU baseline on this host, same inputs, also cross-checking the GPU bit for bit.
 
@@ -578,19 +705,22 @@ def cpu_baseline(rows, seeds, signs, L, gpu_out):
     res = {"value": round(bytes_round / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
            "sample": f"the full workload: {N} rows x {L} slots, {seeds.shape[0]} self-mask seeds; the reference's "
                      "numpy loop (SA_ServiceAgent.py:346-350,530-536,605) over OpenSSL ChaCha20, 1 thread",
-           "seconds": round(dt, 3), "matches_gpu": bool(np.array_equal(out, gpu)),
-           "cpu": platform.processor() or platform.machine()}
+           "seconds": round(dt, 3), "matches_gpu": bool(np.array_equal(out, gpu))}
     t0 = time.perf_counter()
     out_c = O.aggregate_unmask(host, seeds, signs, L=L, threads=1)
     dt_c = time.perf_counter() - t0
     res["c_port_1_thread"] = {"value": round(bytes_round / dt_c / 1e9, 3), "seconds": round(dt_c, 3),
                               "matches_gpu": bool(np.array_equal(out_c, gpu))}
-    threads = min(16, os.cpu_count() or 1)
+    threads, quota = host_threads()
     t0 = time.perf_counter()
     out2 = O.aggregate_unmask(host, seeds, signs, L=L, threads=threads)
     dt2 = time.perf_counter() - t0
     res["c_port_all_cores"] = {"value": round(bytes_round / dt2 / 1e9, 3), "cores": threads,
-                               "seconds": round(dt2, 3), "matches_gpu": bool(np.array_equal(out2, gpu))}
+                               "seconds": round(dt2, 3), "matches_gpu": bool(np.array_equal(out2, gpu)),
+                               "note": "OpenMP over every core this job may use: min(nproc, cgroup CPU quota)"}
+    res["cpu"] = cpu_model()
+    res["nproc"] = os.cpu_count()
+    res["cgroup_cpu_quota_cores"] = quota
     return res
 
 

@@ -28,6 +28,7 @@ fraction: float = P.fraction
 nonce = P.nonce
 
 _engine = None
+_group = None
 _graphs: dict = {}
 _committees: dict = {}
 _pkis: dict = {}
@@ -65,6 +66,35 @@ def engine():
         from ...engine import MaskEngine
         _engine = MaskEngine(int(os.environ.get("FLM_DEVICE", "0")))
     return _engine
+
+
+def server_devices() -> list:
+    """Devices the server's vector steps use: FLM_GROUP_DEVICES ("0,1,2,..."; one id repeated =
+    loopback ranks on one GPU), else FLM_GPUS devices 0..n-1, else every visible GPU."""
+    spec = os.environ.get("FLM_GROUP_DEVICES", "").strip()
+    if spec:
+        return [int(d) for d in spec.split(",")]
+    n = int(os.environ.get("FLM_GPUS", "0"))
+    if n <= 0:
+        from ... import _lib
+        n = max(1, int(_lib.load().flm_device_count()))
+    return list(range(n))
+
+
+def server_engine():
+    """The server's partial sum and unmask (SA_ServiceAgent.py:346-350, 529-605) run on every
+    device of server_devices(): a DeviceGroup (client-sharded rows, slot-sharded masks, one RCCL
+    reduce-scatter) when that is more than one, else the process MaskEngine."""
+    global _group
+    devs = server_devices()
+    if len(devs) == 1 and devs[0] == int(os.environ.get("FLM_DEVICE", "0")):
+        return engine()
+    if _group is None or _group.devices != devs:
+        from ...engine import DeviceGroup
+        if _group is not None:
+            _group.close()
+        _group = DeviceGroup(devs)
+    return _group
 
 
 def committee(num_clients: int) -> set:

@@ -6,11 +6,12 @@ Four-step round state machine, same as the reference (:123-135):
   2 forward_signatures  forward the committee's signed offline set (DEC)
   3 reconstruction      recover m_i from committee shares; unmask; combine
 
-The hot loops are replaced by calls into the MI355X engine:
-  report_process        S = sum_{i in U} y_i         (:346-350)  -> MaskEngine.aggregate_unmask(rows, K=0)
+The hot loops are replaced by calls into the MI355X engine (protocol.server_engine(): every GPU
+of the node through one DeviceGroup, or the one MaskEngine):
+  report_process        S = sum_{i in U} y_i         (:346-350)  -> server_engine().aggregate_unmask(rows, K=0)
   reconstruction_process
       s_ij for dropout pairs: c1 - sum_j lambda_j (sk_j c0), SHA-256   (:542-585) -> MaskEngine.ec_combine_wire
-      out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> MaskEngine.mask_accumulate
+      out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> server_engine().aggregate_unmask([S], seeds)
       m_i for online clients: sum_j lambda_j y_{j,i} mod n      (:506-526) -> MaskEngine.shamir_combine
 The vector arithmetic is bit-exact with the reference's numpy uint32 code.
 Message payloads use the reference's JSON formats (wire.py).
@@ -163,8 +164,8 @@ class SA_ServiceAgent(Agent):
         for cid, v in self.user_vectors.items():
             if len(v) != self.vector_len:
                 raise RuntimeError("Client sends vector of incorrect length.")
-        self.vec_sum_partial = param.engine().aggregate_unmask(list(self.user_vectors.values()), [], [],
-                                                              L=self.vector_len)
+        self.vec_sum_partial = param.server_engine().aggregate_unmask(list(self.user_vectors.values()), [], [],
+                                                                     L=self.vector_len)
         # dropout pairs (online nb, offline id) and their signs (:359-380)
         nbrs = param.neighbors(self.current_iteration, self.num_clients, self.neighborhood_size)
         pairs, signs = P.dropout_pairs(nbrs, online, offline)
@@ -256,9 +257,10 @@ class SA_ServiceAgent(Agent):
             for s, sg in zip(pair_seeds, self.recon_symbol.values()):
                 seeds.append(bytes(s[: self.key_length]))
                 signs.append(sg)
-        # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU
-        out = self.vec_sum_partial.astype(np.uint32, copy=True)
-        self.final_sum = param.engine().mask_accumulate(seeds, signs, out)
+        # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU(s): the partial sum is one
+        # more row, and every device regenerates the K masks over its own slot shard only
+        self.final_sum = param.server_engine().aggregate_unmask([self.vec_sum_partial], seeds, signs,
+                                                                L=self.vector_len)
         self.results[self.current_iteration] = self.final_sum
         self.online_counts[self.current_iteration] = len(self.user_vectors)
         self.agent_print("final sum:", self.final_sum)

@@ -1,0 +1,130 @@
+"""Multi-GPU server reconstruction (BASELINE c5 on G GPUs): seed recovery + unmask, sharded.
+
+SA_ServiceAgent.reconstruction_process (:499-605) on G ranks, one process per GPU.  Every
+rank needs every seed -- it regenerates all K masks over its own slot shard -- so the
+question is who recovers which seeds:
+
+* m_i (Shamir, :506-526): every rank recovers all M of them.  It is one tiny launch
+  (0.06 ms at c5 for M = 4055), cheaper than any exchange.
+* s_ij (threshold ElGamal + SHA-256, :542-585): rank r recovers only pairs
+  [r*Dc, (r+1)*Dc), Dc = ceil(D/G), then ONE all-gather of 32*Dc bytes per rank gives
+  every rank all D keys.  The combine is latency-bound (one scalar multiplication is a
+  ~2.7 ms chain per lane whatever the batch), so the split does not shorten it, but it
+  takes G times fewer lanes on each GPU and runs on a side stream under the self-mask pass.
+
+Per rank, in stream order:
+  side:  ec_combine(my pairs) -> chunk ------------------------------------\\
+  main:  shamir(all m_i) -> rows(my clients) + self masks(my shard) -> part -+-> all_gather(chunk)
+         -> part + pair masks(my shard) -> part2 -> reduce_scatter -> out shard
+
+The two exchanges go through the library's RCCL communicator (flm_all_gather_dev,
+flm_reduce_scatter_dev) when one is attached (distributed.init_rccl), else through
+torch.distributed (gloo on host copies: ranks sharing one GPU in tests).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .distributed import padded_length, shard_bounds
+
+
+def pair_chunk(D: int, world: int, rank: int):
+    """[a, b) of the dropout pairs rank recovers; every rank's chunk is Dc = ceil(D/G) long (padded)."""
+    Dc = (D + world - 1) // world if D else 0
+    a = min(rank * Dc, D)
+    return a, min(a + Dc, D), Dc
+
+
+class ShardedReconstruction:
+    def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None):
+        self.eng = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.L = L
+        self.Lp = padded_length(L, self.world)
+        self.S = self.Lp // self.world
+        self.lo, self.hi = shard_bounds(L, self.world, self.rank)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if comm is None:
+            comm = "rccl" if (self.world > 1 and engine.comm_size() == (self.world, self.rank)) else "torch"
+        self.comm = comm
+        self.side = torch.cuda.Stream(device=self.device)
+        self._bufs = {}
+
+    def _buf(self, name, shape, dtype, fill=None):
+        b = self._bufs.get(name)
+        if b is None or tuple(b.shape) != tuple(shape) or b.dtype != dtype:
+            b = torch.empty(shape, dtype=dtype, device=self.device)
+            if fill is not None:
+                b.fill_(fill)
+            self._bufs[name] = b
+        return b
+
+    def _all_gather(self, chunk, gathered, stream):
+        if self.world == 1:
+            gathered[: chunk.shape[0]].copy_(chunk)
+        elif self.comm == "rccl":
+            self.eng.all_gather_dev(chunk, gathered, stream=stream)
+        else:
+            with torch.cuda.stream(stream):
+                if dist.get_backend(self.group) == "gloo":
+                    host = torch.empty((gathered.shape[0],) + tuple(chunk.shape[1:]), dtype=chunk.dtype)
+                    dist.all_gather_into_tensor(host, chunk.cpu(), group=self.group)
+                    gathered.copy_(host)
+                else:
+                    dist.all_gather_into_tensor(gathered, chunk, group=self.group)
+
+    def _reduce_scatter(self, part, out, stream):
+        if self.world == 1:
+            out[: self.L].copy_(part[: self.L])
+        elif self.comm == "rccl":
+            self.eng.reduce_scatter_dev(part, out, self.S, stream=stream)
+        else:
+            with torch.cuda.stream(stream):
+                if dist.get_backend(self.group) == "gloo":
+                    host = torch.empty(self.S, dtype=part.dtype)
+                    dist.reduce_scatter_tensor(host, part.cpu(), op=dist.ReduceOp.SUM, group=self.group)
+                    out[: self.S].copy_(host)
+                else:
+                    dist.reduce_scatter_tensor(out[: self.S], part, op=dist.ReduceOp.SUM, group=self.group)
+
+    def run(self, rows, lambdas, mi_shares, c1_mine, pair_shares_mine, pair_signs, D: int, out, stream=None):
+        """rows (N_r, pitch) int32: this rank's online clients; lambdas (T, 32); mi_shares (T, M, 32) -- all
+        online clients; c1_mine (Dr, 64), pair_shares_mine (T, Dr, 64): this rank's pair chunk
+        (pair_chunk(D, G, rank)); pair_signs (D,) int8 -- all pairs, recon_symbol order; out (>= S,) int32
+        receives this rank's slots [lo, hi) (world 1: out[:L] is the whole sum).  Enqueued on `stream`."""
+        eng = self.eng
+        main = torch.cuda.current_stream(self.device) if stream is None else stream
+        M = mi_shares.shape[1]
+        _, _, Dc = pair_chunk(D, self.world, self.rank)
+        Dr = c1_mine.shape[0] if c1_mine is not None else 0
+        with torch.cuda.stream(main):
+            m_seeds = self._buf("m_seeds", (M, 32), torch.uint8)
+            neg = self._buf("neg", (M,), torch.int8, -1)
+            chunk = self._buf("chunk", (max(Dc, 1), 32), torch.uint8, 0)
+            gathered = self._buf("gathered", (max(Dc, 1) * self.world, 32), torch.uint8)
+            flags = self._buf("flags", (max(Dr, 1),), torch.int32)
+            part = self._buf("part", (1, self.Lp), torch.int32, 0)
+            part2 = self._buf("part2", (self.Lp,), torch.int32, 0)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        if Dr:
+            self.side.wait_event(ready)
+            eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+        eng.aggregate_unmask_dev(rows, m_seeds, neg, part[0], L=self.L, mask_lo=self.lo, mask_hi=self.hi,
+                                 stream=main)
+        if D:
+            main.wait_event(done)
+            self._all_gather(chunk, gathered, main)
+            eng.aggregate_unmask_dev(part, gathered[:D], pair_signs, part2, L=self.L, mask_lo=self.lo,
+                                     mask_hi=self.hi, stream=main)
+            src = part2
+        else:
+            src = part[0]
+        self._reduce_scatter(src, out, main)
+        return out, flags

@@ -1,0 +1,149 @@
+"""util/flm.py for the reference tree: the ctypes binding a maintainer adds to eniac/flamingo.
+
+Save as ``util/flm.py`` in the reference, then edit the call sites as INTEGRATION.md shows
+(agent/flamingo/SA_ServiceAgent.py:346-350, 506-605; SA_ClientAgent.py:246-324).  It binds
+libflamingo_hip.so directly -- no dependency on the flamingo_amd package -- and mirrors the
+reference's own conventions: uint32 numpy vectors, 32-byte seeds, +-1 signs, EccPoint-like
+objects with .x/.y for the ElGamal and decryption-share points, RuntimeError on failure
+(as SA_ServiceAgent.py:349,502,579,592 raise).
+
+Environment:
+  FLM_LIB      path of libflamingo_hip.so (default: found by the dynamic loader)
+  FLM_DEVICE   the GPU of the single-device context (default 0)
+  FLM_GPUS     > 1: the server's aggregate_unmask runs on devices 0..FLM_GPUS-1 of this one
+               process (flm_group: client-sharded rows, slot-sharded masks, one RCCL
+               reduce-scatter, ncclUint32) -- the reference server is a single DES process
+               (Kernel.py:190-271), so this is how it uses all GPUs of the node.
+The contexts are created lazily, on first use: after SA_ServiceAgent.py:562 forks its
+multiprocessing.Pool, never before.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_lib = ctypes.CDLL(os.environ.get("FLM_LIB", "libflamingo_hip.so"))
+_vp, _int, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+_u8p, _i8p, _u32p, _i64p = (ctypes.POINTER(t) for t in (ctypes.c_uint8, ctypes.c_int8, ctypes.c_uint32,
+                                                         ctypes.c_int64))
+for _name, _res, _args in (
+        ("flm_init", _int, [ctypes.POINTER(_vp), _int]),
+        ("flm_last_error", ctypes.c_char_p, [_vp]),
+        ("flm_aggregate_unmask", _int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),
+        ("flm_client_mask", _int, [_vp, _u32p, _int, _i64p, _u8p, _i8p, _sz, _u32p]),
+        ("flm_shamir_combine", _int, [_vp, _u8p, _u8p, _int, _int, _u8p]),
+        ("flm_ec_combine", _int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint32)]),
+        ("flm_group_init", _int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int)]),
+        ("flm_group_last_error", ctypes.c_char_p, [_vp]),
+        ("flm_group_aggregate_unmask", _int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p])):
+    _f = getattr(_lib, _name)
+    _f.restype, _f.argtypes = _res, _args
+
+_ctx = None
+_group = None
+
+
+def _context():
+    global _ctx
+    if _ctx is None:
+        c = _vp()
+        if _lib.flm_init(ctypes.byref(c), int(os.environ.get("FLM_DEVICE", "0"))):
+            raise RuntimeError(_lib.flm_last_error(None).decode())
+        _ctx = c
+    return _ctx
+
+
+def _server_group():
+    """The process's device group when FLM_GPUS > 1, else None."""
+    global _group
+    n = int(os.environ.get("FLM_GPUS", "1"))
+    if n <= 1:
+        return None
+    if _group is None:
+        g = _vp()
+        if _lib.flm_group_init(ctypes.byref(g), n, None):
+            raise RuntimeError(_lib.flm_group_last_error(None).decode())
+        _group = g
+    return _group
+
+
+def _check(rc, group=None):
+    if rc:
+        msg = _lib.flm_group_last_error(group) if group is not None else _lib.flm_last_error(_ctx)
+        raise RuntimeError(msg.decode())
+
+
+def _seed_arrays(seeds, signs):
+    K = len(seeds)
+    sd = np.frombuffer(b"".join(bytes(s) for s in seeds), np.uint8) if K else np.zeros(32, np.uint8)
+    sg = np.asarray(signs, np.int8) if K else np.ones(1, np.int8)
+    if sd.size != 32 * K or sg.size != max(K, 1):
+        raise RuntimeError("seeds must be 32 bytes each, one sign per seed")
+    return sd, sg, K
+
+
+def aggregate_unmask(vectors, seeds, signs, L):
+    """sum(vectors) + sum_k signs[k] * PRG(seeds[k]) mod 2^32, as uint32[L]
+    (vec_sum_partial + cancel_vec + mi_vec, SA_ServiceAgent.py:346-350, 529-605)."""
+    vecs = [np.ascontiguousarray(v, dtype=np.uint32) for v in vectors]
+    for v in vecs:
+        if v.shape[0] != L:
+            raise RuntimeError("Client sends vector of incorrect length.")
+    rows = (_u32p * max(1, len(vecs)))(*[v.ctypes.data_as(_u32p) for v in vecs])
+    sd, sg, K = _seed_arrays(seeds, signs)
+    out = np.empty(L, np.uint32)
+    g = _server_group()
+    if g is not None:
+        _check(_lib.flm_group_aggregate_unmask(g, rows, len(vecs), sd.ctypes.data_as(_u8p), sg.ctypes.data_as(_i8p),
+                                               K, L, out.ctypes.data_as(_u32p)), g)
+    else:
+        _check(_lib.flm_aggregate_unmask(_context(), rows, len(vecs), sd.ctypes.data_as(_u8p),
+                                         sg.ctypes.data_as(_i8p), K, L, out.ctypes.data_as(_u32p)))
+    return out
+
+
+def _be(ints):
+    """Python ints -> n x 32 big-endian bytes."""
+    return np.frombuffer(b"".join(int(v).to_bytes(32, "big") for v in ints), np.uint8)
+
+
+def shamir_combine(shares_by_member, coeffs):
+    """[(sum_j coeffs[j] * shares_by_member[j][i]) % n .to_bytes(32, 'big') for each i]
+    (the m_i recovery of SA_ServiceAgent.py:517-526)."""
+    T, M = len(coeffs), len(shares_by_member[0])
+    sh = np.concatenate([_be(s) for s in shares_by_member])
+    out = np.empty(M * 32, np.uint8)
+    _check(_lib.flm_shamir_combine(_context(), sh.ctypes.data_as(_u8p), _be(coeffs).ctypes.data_as(_u8p), T, M,
+                                   out.ctypes.data_as(_u8p)))
+    return [out[32 * i:32 * i + 32].tobytes() for i in range(M)]
+
+
+def ec_combine(c1_points, shares_by_member, coeffs):
+    """SHA-256 keys of c1_i - sum_j coeffs[j] * shares_by_member[j][i] (SA_ServiceAgent.py:542-585):
+    EccPoint-like objects (.x, .y) in, 32-byte ChaCha20 keys out."""
+    xy = lambda pts: _be([c for p in pts for c in (int(p.x), int(p.y))])
+    T, D = len(coeffs), len(c1_points)
+    if D == 0:
+        return []
+    sh = np.concatenate([xy(s) for s in shares_by_member])
+    seeds = np.empty(D * 32, np.uint8)
+    _check(_lib.flm_ec_combine(_context(), xy(c1_points).ctypes.data_as(_u8p), sh.ctypes.data_as(_u8p),
+                               _be(coeffs).ctypes.data_as(_u8p), T, D, 1, None, seeds.ctypes.data_as(_u8p), None))
+    return [seeds[32 * i:32 * i + 32].tobytes() for i in range(D)]
+
+
+def client_mask(seeds, signs, L, x=None):
+    """x (default: the all-ones input of SA_ClientAgent.py:304) + sum_k signs[k] * PRG(seeds[k])
+    for one client: the composition of SA_ClientAgent.py:246-324."""
+    seg = np.array([0, len(seeds)], np.int64)
+    sd, sg, K = _seed_arrays(seeds, signs)
+    out = np.empty(L, np.uint32)
+    xp = None
+    if x is not None:
+        x = np.ascontiguousarray(x, dtype=np.uint32)
+        if x.shape != (L,):
+            raise RuntimeError("vector length error")
+        xp = x.ctypes.data_as(_u32p)
+    _check(_lib.flm_client_mask(_context(), xp, 1, seg.ctypes.data_as(_i64p), sd.ctypes.data_as(_u8p),
+                                sg.ctypes.data_as(_i8p), L, out.ctypes.data_as(_u32p)))
+    return out

@@ -14,9 +14,10 @@ imported by the product path.  Restates, in plain affine integer arithmetic:
 
 Pins: tests/test_ec_cpu.py checks this arithmetic against OpenSSL's
 independent P-256 (EC_POINT_mul / EC_POINT_add) and against the group law
-(n*G = infinity, (a+b)G = aG + bG).  The reference's own values cannot be
-reproduced here (pycryptodomex is not installed): parity vs the reference
-itself is UNPINNED, as for the rest of the oracle.
+(n*G = infinity, (a+b)G = aG + bG), and
+tests/test_ref_golden_cpu.py::test_ec_oracle_recovers_reference_seeds checks it
+recovers, from the reference's own decryptors' shares, the exact keys the
+reference's reconstruction_process derived (tests/golden/make_ref_golden.py).
 """
 from __future__ import annotations
 

@@ -23,12 +23,13 @@
  *     :529-536 (self masks, always subtracted), :587-603 (dropout-pair masks,
  *     sign recon_symbol), :538-540/:605 (final combine), all mod 2^32.
  *
- * PARITY UNPINNED against the reference itself: the reference ships no
- * tests or golden vectors, and its cipher (pycryptodomex, un-vendored) is not
- * importable here, so no reference-produced vector exists.  Substitute pins:
- * the published ChaCha20 vectors (RFC 7539 2.3.2 and A.1), fixtures generated
- * with OpenSSL's independent ChaCha20 (tests/golden/make_golden.py), and the
- * protocol invariant out == |U| (SA_ClientAgent.py:304, SA_ServiceAgent.py:605).
+ * PINNED to the reference itself: tests/test_ref_golden_cpu.py compares this
+ * code with rounds the reference's own agents produced (tests/golden/
+ * make_ref_golden.py imports util/param.py and agent/flamingo/SA_*Agent.py from
+ * the reference under a pycryptodomex/libnum stand-in).  Also pinned by the
+ * published ChaCha20 vectors (RFC 7539 2.3.2 and A.1), fixtures generated with
+ * OpenSSL's independent ChaCha20 (tests/golden/make_golden.py), and the protocol
+ * invariant out == |U| (SA_ClientAgent.py:304, SA_ServiceAgent.py:605).
  */
 #include <stdint.h>
 #include <stddef.h>

@@ -21,9 +21,12 @@ Reference call sites restated (paths relative to /root/reference):
 * server aggregate + unmask -- agent/flamingo/SA_ServiceAgent.py:346-350,
   529-540, 587-605.
 
-PARITY UNPINNED against the reference itself (no reference tests/fixtures
-exist and its pycryptodomex cipher is not importable here).  Pinned instead by
-RFC 7539 vectors, OpenSSL-generated fixtures (tests/golden/) and the
+PINNED to the reference itself: tests/test_ref_golden_cpu.py checks these
+functions against fixtures the reference's own agents produced
+(tests/golden/make_ref_golden.py: util/param.py and agent/flamingo imported from
+the reference under a pycryptodomex/libnum stand-in) -- client vectors, the
+server's S / M / C / final_sum, committee, graphs and recon_symbol order.  Also
+pinned by RFC 7539 vectors, OpenSSL-generated fixtures (tests/golden/) and the
 out == |U| protocol invariant; see DESIGN.md section 3.
 """
 from __future__ import annotations

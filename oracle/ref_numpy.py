@@ -8,9 +8,9 @@ It follows the reference's own statements and their cost structure:
   final_sum = vec_sum_partial + cancel_vec + mi_vec                  :605
 The cipher in the reference is pycryptodomex's C ChaCha20 (not installed
 here); this restatement calls OpenSSL's C ChaCha20 (EVP_chacha20, zero IV ==
-the 8-byte zero nonce DJB stream) through ctypes.  PARITY UNPINNED against the
-reference itself; it is checked against the C
-oracle and the GPU result.  Single-threaded, like the reference server.
+the 8-byte zero nonce DJB stream) through ctypes.  It is checked against
+the C oracle and the GPU result, and the C oracle against the reference's own
+rounds (tests/test_ref_golden_cpu.py).  Single-threaded, like the reference server.
 """
 from __future__ import annotations
 

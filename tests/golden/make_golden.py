@@ -7,10 +7,12 @@ flamingo_amd/.  With a zero 16-byte IV (RFC 7539 layout: 32-bit counter +
 that pycryptodomex uses in the reference (util/param.py:32, 64-bit counter)
 for every block index < 2^32, which covers every length used here.
 
-The reference itself cannot be imported here (pycryptodomex is absent and is
-not shimmed), and it ships no fixtures of its own, so parity on this path is
-pinned by published ChaCha20 vectors (tests/test_oracle.py) plus these
-OpenSSL-generated vectors and the protocol invariant out == |U|.
+These vectors are the independent-implementation pin.  The reference's OWN
+code produces the other set: tests/golden/make_ref_golden.py imports
+util/param.py, util/util.py, util/crypto and agent/flamingo/SA_*Agent.py from
+/root/reference under a dependency shim (tests/golden/refshim.py) and records
+whole protocol rounds (ref_golden.json / ref_golden.npz), which
+tests/test_ref_golden_{cpu,gpu}.py compare against the oracle and the HIP path.
 
 Outputs:
   golden.json      -- PRG heads/tails/digests, graph digests, round fixtures

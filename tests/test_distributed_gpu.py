@@ -22,3 +22,18 @@ def test_rccl_async_pipelined_round():
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "ok=True" in r.stdout
+
+
+@pytest.mark.parametrize("nproc,backend", [(1, "nccl"), (2, "gloo"), (3, "gloo")])
+def test_sharded_reconstruction(nproc, backend):
+    """flamingo_amd.dist_recon on 1 (library RCCL communicator) and 2/3 ranks (gloo, one GPU)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tools", "dist_recon_smoke.py"), backend]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "sharded reconstruction ok=True" in r.stdout
