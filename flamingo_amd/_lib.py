@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libflamingo_hip.so")
+# FLM_LIB_PATH: load another build of the same sources (tools/sanitize.sh's ASan/UBSan host build)
+LIB_PATH = os.environ.get("FLM_LIB_PATH") or os.path.join(HERE, "lib", "libflamingo_hip.so")
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _i8p = ctypes.POINTER(ctypes.c_int8)

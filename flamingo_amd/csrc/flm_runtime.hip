@@ -106,7 +106,7 @@ struct flm_ctx {
     int table_k = -1;  // seeds in the current device seed table
     int tune_variant = -1;   // items_kernel variant, -1 = auto
     int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
-    int tune_min_items = 1024;  // planner target for work items per aggregate launch
+    int tune_min_items = 1024;  // planner target for work items per aggregate launch (kDefaultMinItems)
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
@@ -287,6 +287,9 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
     return 0;
 }
 
+constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
+constexpr uint64_t kUnsplitTiles = 256;  // MI355X CUs: from this many tiles a round is not split
+
 // Host-only planning of one aggregate round (no device state): fills `items`
 // and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
 // diagnostic entry point.
@@ -310,7 +313,16 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     const uint64_t tr = N > 0 ? (L + W - 1) / W : 0;
     const uint64_t tm = (K > 0 && mask_hi > mask_lo) ? (mask_hi - mask_lo + W - 1) / W : 0;
     int pr, pm;
-    choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)min_items);
+    if (!seed_light && min_items == kDefaultMinItems && mask_lo == 0 && mask_hi == L && tr == tm &&
+        tm >= kUnsplitTiles) {
+        // A whole-vector ChaCha-heavy round with at least one tile per CU: one item per tile, rows and
+        // seeds unsplit -- no atomics, no zero-fill, one LDS combine per tile.  BASELINE c3 (N=1024,
+        // L=2^18: 256 tiles) ran 0.434 ms as 1024 items (4 seed parts) and 0.396 ms as 256
+        // (profiles/r02_ab_c3.log); c4 / c5 (1024 tiles) are unsplit either way.
+        pr = pm = 1;
+    } else {
+        choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)min_items);
+    }
     plan.subtiles = subtiles;
     plan.seed_light = seed_light;
     plan_job(j, pitch, subtiles, pr, pm, pairing == 1, items, plan.needs_zero, plan.atomics, plan.single_tile);

@@ -19,7 +19,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flamingo_amd import MaskEngine  # noqa: E402
 
-VARIANTS = {"coalesced": 0, "block": 1, "merged": 2, "merged_w8": 3, "merged_ru4": 4, "merged_nt": 5,
+VARIANTS = {"auto": -1, "coalesced": 0, "block": 1, "merged": 2, "merged_w8": 3, "merged_ru4": 4, "merged_nt": 5,
             "merged_ru4_nt": 6, "merged_spread": 7, "block_spread": 8}
 
 
