@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--clients-per-gpu", type=int, default=1024)
     ap.add_argument("--log2-L", type=int, default=20)
     ap.add_argument("--dropout", type=float, default=0.0, help="fraction of clients offline (c5: 0.01)")
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="untimed rounds before the warm-up until this much GPU time has passed: MI355X ramps its "
+                         "clock over ~100 ms of load (tools/tail_probe.py, DESIGN.md section 6)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-copy", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")
@@ -160,6 +163,12 @@ def main():
         return rnd.launch(rows_on, d_seeds, d_signs, stream)
 
     ev_k = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    def agree_max(n):
+        t = torch.tensor([n], dtype=torch.int64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
+    settle = settle_clock(torch, step, stream, args.settle_ms, agree=agree_max if G > 1 else None)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -210,6 +219,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u32", "correct": ok,
+        "clock_settle": settle,
         "data": "synthetic: valid masked rows y_i = 1 + PRG(m_i) +- PRG(s_ij) made on-GPU from SHA-256 bench "
                 "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
         "config": {"workload": "c4: aggregate + self-mask and dropout-pair unmask, one server round",
@@ -271,6 +281,7 @@ def main():
     return 0 if ok else 1
 
 
+SETTLE_CONFIG_MS = 100.0  # clock settle before each config's first iteration (settle_clock)
 RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-split schedule (recon_probe sweep:
                           # 24 of MI355X's 256); a multiple of the 8 XCDs so every XCD loses the same count
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
@@ -278,6 +289,35 @@ RECON_QUEUE_MIN_ITEMS = 1024  # its pass 1 plan: single-tile items, the 57-VGPR 
                              # (8.94 ms vs 9.08 at 4096 and 9.42 at 2048; profiles/r01_recon_queue_minitems.log)
 RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 24 / 32 / 40 CUs ->
                                 # 9.97 / 9.75 / 11.05 ms at c5; profiles/r01_recon_queue_sweep.log)
+
+
+def settle_clock(torch, step, stream, ms, agree=None):
+    """Untimed rounds, back to back, for about `ms` of GPU time (before the W warm-up steps).
+    An MI355X coming off host-side preparation runs its first launches at a lower clock and takes
+    ~100 ms of load to settle (profiles/r02_tail_probe.log: c4 launches flat at 1.42 ms after it;
+    profiles/r01_c4_launch_series.log: 2.2 -> 1.68 ms over the first ~30 ms, pre-lockstep).
+    The round count comes from the first 5 rounds' time; `agree` (multi-GPU: max over ranks)
+    makes every rank run the same count, since each round ends in a collective."""
+    if ms <= 0:
+        return {"ms": 0.0, "rounds": 0}
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(5):
+        step()
+    e1.record(stream)
+    e1.synchronize()
+    per = max(e0.elapsed_time(e1) / 5, 1e-3)
+    n = max(5, int(ms / per + 0.999))
+    if agree is not None:
+        n = agree(n)
+    for _ in range(n - 5):
+        step()
+    e2 = torch.cuda.Event(enable_timing=True)
+    e2.record(stream)
+    e2.synchronize()
+    return {"ms": round(e0.elapsed_time(e2), 1), "rounds": n,
+            "what": "untimed rounds before the warm-up so the clock settles (outside the timed region)"}
 
 
 def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, check_oracle=False, recovery=False):
@@ -336,8 +376,8 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         cm_ms.append(c0.elapsed_time(c1))
         cm_words.append(int(seg[-1]) * L)
         r_on = rows if len(on) == N else rows[torch.from_numpy(on).to(dev)].contiguous()
-        for _ in range(2):
-            eng.aggregate_unmask_dev(r_on, d_s, d_g, out, L=L, stream=stream)
+        settle_clock(torch, lambda: eng.aggregate_unmask_dev(r_on, d_s, d_g, out, L=L, stream=stream), stream,
+                     SETTLE_CONFIG_MS if it == 1 else 10.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(steps):

@@ -28,11 +28,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", OUT + ".tmp"] + SRC
+    # one hipcc per source, in parallel, then one link (the P-256 and kernel files dominate)
+    objs = [os.path.join(os.path.dirname(OUT), os.path.basename(s) + ".o") for s in SRC]
+    procs = []
+    for s, o in zip(SRC, objs):
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", "-o", o, s]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), cmd))
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

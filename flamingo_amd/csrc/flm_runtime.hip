@@ -171,9 +171,12 @@ void plan_job(const Job &j, uint64_t pitch, int subtiles, int parts_r, int parts
     }
     // A tile written by exactly one Item is stored; otherwise every contributor
     // adds atomically into a zeroed output.  Rows and masks share one Item per
-    // tile ("same tile") only in the unsplit whole-vector case.
+    // tile ("same tile") in whole-vector rounds whose rows and seeds are cut into
+    // the same number of parts: unit i of each list then covers the same tile, and
+    // the item keeps the merged single-accumulator kernel (atomic when parts > 1).
     const bool both = !R.empty() && !M.empty();
-    const bool paired_same = both && parts_r == 1 && parts_m == 1 && j.mask_lo == 0 && j.mask_hi == j.L;
+    bool paired_same = both && parts_r == parts_m && j.mask_lo == 0 && j.mask_hi == j.L && R.size() == M.size();
+    for (size_t i = 0; paired_same && i < R.size(); ++i) paired_same = R[i].tile == M[i].tile;
     const bool atomic = parts_r > 1 || parts_m > 1 || (both && !paired_same);
     if (atomic) needs_zero = true;
     if (R.empty() && (j.mask_lo > 0 || j.mask_hi < j.L || M.empty())) needs_zero = true;
@@ -288,7 +291,8 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
 }
 
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
-constexpr uint64_t kUnsplitTiles = 256;  // MI355X CUs: from this many tiles a round is not split
+constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this many a whole-vector round is not split
+constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
 
 // Host-only planning of one aggregate round (no device state): fills `items`
 // and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
@@ -313,13 +317,17 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     const uint64_t tr = N > 0 ? (L + W - 1) / W : 0;
     const uint64_t tm = (K > 0 && mask_hi > mask_lo) ? (mask_hi - mask_lo + W - 1) / W : 0;
     int pr, pm;
-    if (!seed_light && min_items == kDefaultMinItems && mask_lo == 0 && mask_hi == L && tr == tm &&
-        tm >= kUnsplitTiles) {
-        // A whole-vector ChaCha-heavy round with at least one tile per CU: one item per tile, rows and
-        // seeds unsplit -- no atomics, no zero-fill, one LDS combine per tile.  BASELINE c3 (N=1024,
-        // L=2^18: 256 tiles) ran 0.434 ms as 1024 items (4 seed parts) and 0.396 ms as 256
-        // (profiles/r02_ab_c3.log); c4 / c5 (1024 tiles) are unsplit either way.
+    if (!seed_light && min_items == kDefaultMinItems && mask_lo == 0 && mask_hi == L && tr == tm && tm > 0) {
+        // A whole-vector ChaCha-heavy round: rows and seeds are cut into the same number of parts P,
+        // so part p of both lands in one item and the merged single-accumulator kernel runs
+        // (plan_job).  From kUnsplitTiles tiles (4 per CU: c4 / c5, 1024 tiles) one item per tile --
+        // no atomics, no zero-fill; 2048 items measured no faster there.  Fewer tiles (c3, N=1024,
+        // L=2^18: 256 tiles) are split until kSplitItems items: 0.389 ms at P=8 against 0.414 ms
+        // unsplit (one 4-wave/SIMD generation) and 0.410 at P=2 (profiles/r02_ab_split.log).
         pr = pm = 1;
+        while (tm < kUnsplitTiles && tm * (uint64_t)pr < kSplitItems && (uint64_t)pr * 2 * 16 <= (uint64_t)N &&
+               (uint64_t)pr * 2 * 16 <= (uint64_t)K)
+            pr = pm = pr * 2;
     } else {
         choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)min_items);
     }

@@ -54,7 +54,8 @@ def test_c3_full_size(eng):
     o_ = out.cpu().numpy().view(np.uint32)
     assert np.all(o_ == N), np.flatnonzero(o_ != N)[:8]
     plan = eng.last_plan()
-    assert plan["atomics"] == 0 and plan["items"] == 256       # one item per tile (planner rule)
+    # planner rule: 256 tiles split into 8 row/seed parts, same-tile merged items with atomics
+    assert plan["atomics"] == 1 and plan["items"] == 2048 and plan["variant"] == 2
     for (a, n), want in oracle_windows(rows, ss, sg, L, [(0, 2048), (L // 2 + 1024, 1024), (L - 4096, 4096)]):
         assert np.array_equal(o_[a:a + n], want), a
 

@@ -33,6 +33,8 @@ def plan(N, K, L, lo=0, hi=None, pitch=None, prg_slot0=0, subtiles=0, pairing=1)
 
 @pytest.mark.parametrize("N,K,L,lo,hi,pairing", [
     (1024, 1024, 1 << 20, 0, None, 1),          # c4, one GPU
+    (1024, 1024, 1 << 18, 0, None, 1),          # c3: 256 tiles split into 8 same-tile parts
+    (1024, 1000, 1 << 18, 0, None, 1),          # c3 with dropouts (K != N)
     (1024, 204, 1 << 20, 0, None, 1),           # pairs-only
     (1024, 8192, 1 << 20, 3 << 17, 4 << 17, 1),  # rank 3 of 8
     (1024, 8192, 1 << 20, 3 << 17, 4 << 17, 0),  # interleaved items
@@ -104,6 +106,9 @@ def test_plan_covers_everything_once(N, K, L, lo, hi, pairing):
 def test_plan_modes():
     _, f, _ = plan(1024, 1024, 1 << 20)
     assert f & 4 and not f & 2 and (f >> 8) == 1          # single tile, stores, 1024-slot tiles
+    items, f, _ = plan(1024, 1024, 1 << 18)
+    assert f & 4 and f & 2 and f & 1 and len(items) == 2048  # c3: same-tile parts, atomics
+    assert all(int(it["flags"]) & SAME for it in items)
     _, f, _ = plan(1024, 204, 1 << 20)
     assert f & 8 and (f >> 8) == 4                         # seed-light: 4096-slot tiles
     _, f, _ = plan(1024, 8192, 1 << 20, 0, 1 << 17)
