@@ -39,28 +39,63 @@ namespace flm {
     a += b; d ^= a; d = FLM_ROTL(d, 8);           \
     c += d; b ^= c; b = FLM_ROTL(b, 7);
 
-// Rounds 2..10 as inline asm, the four quarter rounds of a half round in lockstep: each of the
-// QR's 12 steps issues for all four QRs back to back (4 adds, 4 xors, 4 rotates, ...).  gfx950
-// issues v_add_u32 / v_xor_b32 in about 2 cycles and v_alignbit_b32 in about 4; left to the
-// compiler, the rotates land between the adds and xors and the whole stream runs at ~4.0 cycles
-// per instruction.  Grouped like this, QR streams measured 3.52 (tools/issue_probe.hip,
-// profiles/r01_issue_probe.log).  One asm statement per instruction, volatile so the order holds.
-#define FLM_A(x, y) asm volatile("v_add_u32 %0, %1, %0" : "+v"(x) : "v"(y))
-#define FLM_X(x, y) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x) : "v"(y))
-#define FLM_R(x, s) asm volatile("v_alignbit_b32 %0, %0, %0, " #s : "+v"(x))  // rotl(x, 32 - s)
-#define FLM_QR4(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3)               \
-    FLM_A(a0, b0); FLM_A(a1, b1); FLM_A(a2, b2); FLM_A(a3, b3);                             \
-    FLM_X(d0, a0); FLM_X(d1, a1); FLM_X(d2, a2); FLM_X(d3, a3);                             \
-    FLM_R(d0, 16); FLM_R(d1, 16); FLM_R(d2, 16); FLM_R(d3, 16);                             \
-    FLM_A(c0, d0); FLM_A(c1, d1); FLM_A(c2, d2); FLM_A(c3, d3);                             \
-    FLM_X(b0, c0); FLM_X(b1, c1); FLM_X(b2, c2); FLM_X(b3, c3);                             \
-    FLM_R(b0, 20); FLM_R(b1, 20); FLM_R(b2, 20); FLM_R(b3, 20);                             \
-    FLM_A(a0, b0); FLM_A(a1, b1); FLM_A(a2, b2); FLM_A(a3, b3);                             \
-    FLM_X(d0, a0); FLM_X(d1, a1); FLM_X(d2, a2); FLM_X(d3, a3);                             \
-    FLM_R(d0, 24); FLM_R(d1, 24); FLM_R(d2, 24); FLM_R(d3, 24);                             \
-    FLM_A(c0, d0); FLM_A(c1, d1); FLM_A(c2, d2); FLM_A(c3, d3);                             \
-    FLM_X(b0, c0); FLM_X(b1, c1); FLM_X(b2, c2); FLM_X(b3, c3);                             \
-    FLM_R(b0, 25); FLM_R(b1, 25); FLM_R(b2, 25); FLM_R(b3, 25);
+// Rounds 2..10 as ONE inline-asm statement per half round: the four quarter rounds in lockstep
+// (each of the QR's 12 steps issues for all four QRs back to back: 4 adds, 4 xors, 4 rotates,
+// ...), and an s_nop after every rotate.  gfx950 issues v_add_u32 / v_xor_b32 in about 2 cycles
+// and the v_alignbit_b32 rotate in about 4 (profiles/r01_isa_probe3.log); a wave that issues a
+// rotate right behind another rotate, or right before the add that reads it, holds up the SIMD
+// for the other waves.  Measured on the c4 mask-only launch (tools/ab_variants.sh,
+// profiles/r02_ab_nops.log; 1024 seeds x 2^20 slots, 8 waves/SIMD):
+//   one asm statement per instruction (round 1: the compiler then pads each statement boundary
+//   where the next reads what the previous wrote with an s_nop 0, i.e. after every group of 4)  1.426 ms
+//   one statement, no s_nop                                                                      1.60
+//   one statement, s_nop 0 after every group of 4                                                1.394
+//   one statement, s_nop 0 after every rotate (and after every group)                            1.297
+//   one statement, s_nop 1 after each of the first three rotates, s_nop 2 after the fourth,
+//   nothing between the adds and xors (FLM_GAP_* defaults below)                                 1.176
+// Gaps between simple ops cost time; gaps after rotates buy it.  The gap macros stay
+// overridable (-DFLM_GAP_...) for tools/build_variants.sh.
+#ifndef FLM_GAP_A1
+#define FLM_GAP_A1 ""  // between the 2nd and 3rd add of a step
+#endif
+#ifndef FLM_GAP_AX
+#define FLM_GAP_AX ""  // adds -> xors
+#endif
+#ifndef FLM_GAP_X1
+#define FLM_GAP_X1 ""  // between the 2nd and 3rd xor
+#endif
+#ifndef FLM_GAP_XR
+#define FLM_GAP_XR ""  // xors -> rotates
+#endif
+#ifndef FLM_GAP_R0
+#define FLM_GAP_R0 "s_nop 1\n\t"  // after the 1st rotate
+#endif
+#ifndef FLM_GAP_R1
+#define FLM_GAP_R1 "s_nop 1\n\t"  // after the 2nd rotate
+#endif
+#ifndef FLM_GAP_R2
+#define FLM_GAP_R2 "s_nop 1\n\t"  // after the 3rd rotate
+#endif
+#ifndef FLM_GAP_RA
+#define FLM_GAP_RA "s_nop 2\n\t"  // after the 4th rotate, before the adds that read them
+#endif
+#define FLM_S_A(a, b) "v_add_u32 %[" #a "], %[" #b "], %[" #a "]\n\t"
+#define FLM_S_X(a, b) "v_xor_b32 %[" #a "], %[" #b "], %[" #a "]\n\t"
+#define FLM_S_R(a, s) "v_alignbit_b32 %[" #a "], %[" #a "], %[" #a "], " #s "\n\t"  // rotl(a, 32 - s)
+// one QR step for QRs 0..3: a += b; d ^= a; d = rotl(d, 32 - s)
+#define FLM_S_STEP(a, b, c, d, s)                                                                       \
+    FLM_S_A(a##0, b##0) FLM_S_A(a##1, b##1) FLM_GAP_A1 FLM_S_A(a##2, b##2) FLM_S_A(a##3, b##3) FLM_GAP_AX \
+    FLM_S_X(d##0, a##0) FLM_S_X(d##1, a##1) FLM_GAP_X1 FLM_S_X(d##2, a##2) FLM_S_X(d##3, a##3) FLM_GAP_XR \
+    FLM_S_R(d##0, s) FLM_GAP_R0 FLM_S_R(d##1, s) FLM_GAP_R1 FLM_S_R(d##2, s) FLM_GAP_R2 FLM_S_R(d##3, s)  \
+    FLM_GAP_RA
+// QR(a_i, b_i, c_i, d_i) for i = 0..3: steps (a,b,d,16) (c,d,b,12) (a,b,d,8) (c,d,b,7)
+#define FLM_QR4(A0, B0, C0, D0, A1, B1, C1, D1, A2, B2, C2, D2, A3, B3, C3, D3)                   \
+    asm volatile(FLM_S_STEP(a, b, c, d, 16) FLM_S_STEP(c, d, a, b, 20) FLM_S_STEP(a, b, c, d, 24)  \
+                 FLM_S_STEP(c, d, a, b, 25)                                                     \
+                 : [a0] "+v"(A0), [b0] "+v"(B0), [c0] "+v"(C0), [d0] "+v"(D0), [a1] "+v"(A1),   \
+                   [b1] "+v"(B1), [c1] "+v"(C1), [d1] "+v"(D1), [a2] "+v"(A2), [b2] "+v"(B2),   \
+                   [c2] "+v"(C2), [d2] "+v"(D2), [a3] "+v"(A3), [b3] "+v"(B3), [c3] "+v"(C3),   \
+                   [d3] "+v"(D3))
 
 // ------------------------------------------------------------------ seeds
 // One thread per seed builds its SeedRec from the raw 32 seed bytes and sign.
@@ -536,16 +571,27 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
             uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
             uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
             uint32_t x12 = ctr, x13 = 0u, x14 = 0u, x15 = 0u;
+            if constexpr (SEG) {
+                // client masking: throughput-bound, the tuned lockstep rounds (FLM_QR4)
 #pragma unroll
-            for (int r = 0; r < 10; ++r) {
-                FLM_QR(x0, x4, x8, x12);
-                FLM_QR(x1, x5, x9, x13);
-                FLM_QR(x2, x6, x10, x14);
-                FLM_QR(x3, x7, x11, x15);
-                FLM_QR(x0, x5, x10, x15);
-                FLM_QR(x1, x6, x11, x12);
-                FLM_QR(x2, x7, x8, x13);
-                FLM_QR(x3, x4, x9, x14);
+                for (int r = 0; r < 10; ++r) {
+                    FLM_QR4(x0, x4, x8, x12, x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15);
+                    FLM_QR4(x0, x5, x10, x15, x1, x6, x11, x12, x2, x7, x8, x13, x3, x4, x9, x14);
+                }
+            } else {
+                // a small round (c2) is one block per lane on a latency path: the s_nop gaps of
+                // FLM_QR4 only lengthen it (7.4 -> 9.4 us per c2 round), so the compiler's order
+#pragma unroll
+                for (int r = 0; r < 10; ++r) {
+                    FLM_QR(x0, x4, x8, x12);
+                    FLM_QR(x1, x5, x9, x13);
+                    FLM_QR(x2, x6, x10, x14);
+                    FLM_QR(x3, x7, x11, x15);
+                    FLM_QR(x0, x5, x10, x15);
+                    FLM_QR(x1, x6, x11, x12);
+                    FLM_QR(x2, x7, x8, x13);
+                    FLM_QR(x3, x4, x9, x14);
+                }
             }
             acc[0] += (x0 + kSigma0) ^ xc;
             acc[1] += (x1 + kSigma1) ^ xc;
@@ -639,14 +685,8 @@ __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t
     uint32_t x12 = (uint32_t)blk, x13 = (uint32_t)(blk >> 32), x14 = n0, x15 = n1;
     const uint32_t i12 = x12, i13 = x13;
     for (int r = 0; r < 10; ++r) {
-        FLM_QR(x0, x4, x8, x12);
-        FLM_QR(x1, x5, x9, x13);
-        FLM_QR(x2, x6, x10, x14);
-        FLM_QR(x3, x7, x11, x15);
-        FLM_QR(x0, x5, x10, x15);
-        FLM_QR(x1, x6, x11, x12);
-        FLM_QR(x2, x7, x8, x13);
-        FLM_QR(x3, x4, x9, x14);
+        FLM_QR4(x0, x4, x8, x12, x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15);
+        FLM_QR4(x0, x5, x10, x15, x1, x6, x11, x12, x2, x7, x8, x13, x3, x4, x9, x14);
     }
     const uint32_t ks[16] = {x0 + kSigma0, x1 + kSigma1, x2 + kSigma2, x3 + kSigma3,
                              x4 + k0,      x5 + k1,      x6 + k2,      x7 + k3,
