@@ -25,6 +25,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--cpu-sample", type=int, default=100, help="scalar mults timed on the host")
 ap.add_argument("--threads", type=int, default=64)
 ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
+ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
 a = ap.parse_args()
 
 rng = random.Random(1)
@@ -45,7 +46,11 @@ lam_t = torch.from_numpy(C.scalars_to_wire(lams)).to(dev)
 seeds = torch.empty((a.D, 32), dtype=torch.uint8, device=dev)
 pts = torch.empty((a.D, 64), dtype=torch.uint8, device=dev)
 flags = torch.empty(a.D, dtype=torch.int32, device=dev)
-s = torch.cuda.Stream()
+if a.cus:
+    from flamingo_amd.reconstruct import pick_cus
+    s = eng.cu_stream(pick_cus(eng.cu_count(), a.cus, "first"))
+else:
+    s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     eng.ec_combine_dev(c1_t, sh_t, lam_t, seeds, flags, points_out=pts, stream=s)
     s.synchronize()
@@ -68,7 +73,7 @@ t = time.perf_counter()
 for i in range(a.cpu_sample):
     C.mul(lams[i % a.T], base[i % 64])
 cpu_per_mul = (time.perf_counter() - t) / a.cpu_sample
-print(json.dumps({"threads": a.threads, "D": a.D, "T": a.T, "scalars": a.scalars, "lambda_hex": [hex(x)[:12] for x in lams[:4]], "gpu_ms": round(gpu_ms, 4),
+print(json.dumps({"lib": os.environ.get("FLM_LIB_PATH", "default"), "cus": a.cus, "threads": a.threads, "D": a.D, "T": a.T, "scalars": a.scalars, "lambda_hex": [hex(x)[:12] for x in lams[:4]], "gpu_ms": round(gpu_ms, 4),
                   "gpu_scalar_mults_per_s": round(a.D * a.T / gpu_ms * 1e3),
                   "cpu_openssl_ms_est": round(cpu_per_mul * a.D * a.T * 1e3, 1),
                   "cpu_openssl_us_per_mul": round(cpu_per_mul * 1e6, 1), "cpu_cores": 1}))
