@@ -29,10 +29,7 @@ struct SeedRec {
     uint32_t col1[4];  // x1, x5, x9, x13 after round-1 column QR(1,5,9,13)
     uint32_t col2[4];  // x2, x6, x10, x14 after QR(2,6,10,14)
     uint32_t col3[4];  // x3, x7, x11, x15 after QR(3,7,11,15)
-    uint32_t d1a;      // x1 + x6   (first step of diagonal QR(1,6,11,12))
-    uint32_t d2a;      // x2 + x7   (first step of diagonal QR(2,7,8,13))
-    uint32_t d2d;      // rotl(x13 ^ d2a, 16)
-    uint32_t pad[7];
+    uint32_t pad[10];
 };
 static_assert(sizeof(SeedRec) == 128, "SeedRec must be 128 bytes");
 
