@@ -291,10 +291,10 @@ SETTLE_CONFIG_MS = 100.0  # clock settle before each config's first iteration (s
 RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-split schedule (recon_probe sweep:
                           # 24 of MI355X's 256); a multiple of the 8 XCDs so every XCD loses the same count
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
-RECON_QUEUE_MIN_ITEMS = 1024  # its pass 1 plan: single-tile items, the 57-VGPR merged variant at 8 waves/SIMD
-                             # (8.94 ms vs 9.08 at 4096 and 9.42 at 2048; profiles/r01_recon_queue_minitems.log)
-RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 24 / 32 / 40 CUs ->
-                                # 9.97 / 9.75 / 11.05 ms at c5; profiles/r01_recon_queue_sweep.log)
+RECON_QUEUE_MIN_ITEMS = 4096  # its pass 1 plan: 4 same-tile row/seed parts per tile (merged kernel, atomics):
+                             # 8.17 ms vs 8.28 at 1024 items (profiles/r02_recon_minitems.log)
+RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 16 / 24 / 32 / 40 / 48 CUs ->
+                                # 11.0 / 9.52 / 8.65 / 9.28 / 9.52 ms at c5; profiles/r02_recon_sweep.log)
 
 
 def settle_clock(torch, step, stream, ms, agree=None):
