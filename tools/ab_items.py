@@ -46,9 +46,14 @@ def main():
     torch.cuda.set_stream(s)
     res = []
     for wl in args.workloads.split(","):
-        K = {"full": 1024, "pairs": 204, "shard8": 8192, "rows": 0, "c3": 1024}[wl]
+        K = 1024 if wl.startswith("strong") else {"full": 1024, "pairs": 204, "shard8": 8192, "rows": 0, "c3": 1024}[wl]
         Lw = (1 << 18) if wl == "c3" else L        # c3: N=1024, L=2^18 (BASELINE configs[2])
         lo, hi = (0, Lw) if wl != "shard8" else (3 * L // 8, 4 * L // 8)
+        rows_w = rows
+        if wl.startswith("strong"):                # one rank of the strong-scaled c4 round: N/G rows, last shard
+            G = int(wl[6:])
+            rows_w = rows[: N // G]
+            lo, hi = (G - 1) * L // G, L
         seeds = torch.randint(0, 256, (max(K, 1), 32), dtype=torch.uint8, device="cuda", generator=g)[:K]
         signs = (torch.randint(0, 2, (max(K, 1),), device="cuda", generator=g) * 2 - 1).to(torch.int8)[:K]
         eng.seed_table_dev(seeds, signs, stream=s)
@@ -59,7 +64,7 @@ def main():
             e0.record(s)
             while t_end < args.settle_ms:
                 for _ in range(10):
-                    eng.aggregate_dev(rows, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)
+                    eng.aggregate_dev(rows_w, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e1.record(s)
                 torch.cuda.synchronize()
@@ -72,11 +77,11 @@ def main():
                 eng.set_tuning("subtiles", st)
                 eng.set_tuning("pairing", pa)
                 eng.set_tuning("min_items", mi)
-                eng.aggregate_dev(rows, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)  # warm / plan
+                eng.aggregate_dev(rows_w, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)  # warm / plan
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
                 e[0].record(s)
                 for r in range(args.reps):
-                    eng.aggregate_dev(rows, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)
+                    eng.aggregate_dev(rows_w, K, out, L=Lw, mask_lo=lo, mask_hi=hi, stream=s)
                     e[r + 1].record(s)
                 torch.cuda.synchronize()
                 ms = [e[i].elapsed_time(e[i + 1]) for i in range(args.reps)]
@@ -89,7 +94,8 @@ def main():
                 plans[(v, st, pa, mi)] = eng.last_plan()
         for (v, st, pa, mi), ms in times.items():
             med, mn = float(np.median(ms)), float(np.min(ms))
-            gbs = (4.0 * N * Lw + 4.0 * Lw) / (med * 1e-3) / 1e9
+            nrw = N // int(wl[6:]) if wl.startswith("strong") else N
+            gbs = (4.0 * nrw * Lw + 4.0 * Lw) / (med * 1e-3) / 1e9
             r = {"workload": wl, "variant": v, "subtiles": st, "pairing": pa, "min_items": mi,
                  "items": plans[(v, st, pa, mi)]["items"], "median_ms": round(med, 4), "min_ms": round(mn, 4),
                  "GB/s": round(gbs, 1)}
