@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void chacha20_xor_kernel(uint32_t k0, uint32_t
 // Units are chunk-major (consecutive claims hit different tiles); each lane makes ChaCha
 // block `tile*64 + lane`, the 16 words go through LDS so that every u32 atomic add of the
 // wave covers 64 consecutive slots.
-constexpr int kUnitSeeds = 16;
+constexpr int kUnitSeeds = 16;  // 32 and 64 measured the same at c5 (profiles/r02_ab_pair_units.log)
 
 template <bool SIDE>
 __global__ __launch_bounds__(64) void pair_units_kernel(const SeedRec *__restrict__ recs, int K,
@@ -733,15 +733,17 @@ __global__ __launch_bounds__(64) void pair_units_kernel(const SeedRec *__restric
 #pragma unroll
         for (int i = 0; i < 16; ++i) lds[lane * 17 + i] = m[i] + nneg;
         __syncthreads();
+        // one address per lane, the 16 stores at immediate offsets j * 256 B; the tile's valid
+        // slot count bounds them (full tiles: all 1024)
         const uint64_t base = (uint64_t)tile * 1024u;
+        const uint32_t valid = (uint32_t)min<uint64_t>(1024u, L - base);
+        // slot e = j*64 + lane sits at lds[(e >> 4) * 17 + (e & 15)] = lds[lb + 68 j]
+        uint32_t *p = dst + base + lane;
+        const uint32_t lb = (uint32_t)(lane >> 4) * 17u + (uint32_t)(lane & 15);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int e = j * 64 + lane;
-            const uint64_t slot = base + (uint64_t)e;
-            if (slot < L)
-                __hip_atomic_fetch_add(&dst[slot], lds[(e >> 4) * 17 + (e & 15)], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int j = 0; j < 16; ++j)
+            if ((uint32_t)(j * 64 + lane) < valid)
+                __hip_atomic_fetch_add(p + j * 64, lds[lb + 68 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
