@@ -607,6 +607,267 @@ __global__ __launch_bounds__(TPB, WPE) void ec_mul_kernel(const uint8_t *__restr
     store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
 }
 
+// ------------------------------------------------ cooperative scalar multiplication
+// The same product as ec_mul_kernel, with FOUR waves (on the CU's four SIMDs) per 64 scalar
+// multiplications: lane l of every wave works on item g = blockIdx.x * 64 + l, and the field
+// multiplications of each point doubling are spread over the waves, exchanging field elements
+// through LDS between three barriers:
+//   L1  w0: delta = Z^2          w1: gamma = Y^2          w2: s = (Y+Z)^2
+//   L2  w0: t = (X-delta)(X+delta)  w1: beta = X gamma   w2: gamma^2, Z3 = s - gamma - delta
+//   L3  w0: X3 = (3t)^2 - 8 beta, Y3 = 3t (4 beta - X3) - 8 gamma^2
+// so a doubling costs 4 multiplications of latency instead of 8 (dbl-2001-b, a = -3).  Additions
+// (~43 per scalar) run on wave 0 with the table of odd multiples in LDS.  A scalar multiplication is
+// one lane's latency chain (~2,850 field multiplications), so where the batch leaves most SIMDs
+// idle -- seed recovery on the whole chip, one rank's share of the pairs on G GPUs, the agents'
+// ECDH/ElGamal batches -- this halves it; where the batch already fills its CUs (the CU-split
+// reconstruction) the per-lane kernel issues fewer instructions.  Exceptional cases as jac_add.
+constexpr int kCoopWaves = 4;
+constexpr int kCoopSlots = 11;
+
+__device__ __forceinline__ void xput(uint32_t *slot, const Fe &a, int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) slot[k * 64 + lane] = a.v[k];
+}
+__device__ __forceinline__ Fe xget(const uint32_t *slot, int lane) {
+    Fe a;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.v[k] = slot[k * 64 + lane];
+    return a;
+}
+
+// acc = 2 acc in every wave (all four waves hold acc; wave-uniform branches on w)
+__device__ __forceinline__ void coop_dbl(Jac &acc, int w, int lane, uint32_t *S) {
+    Fe d, g, sq, t;
+    if (w == 0) {
+        d = fe_sqr(acc.Z);
+        xput(S + 0 * 512, d, lane);
+    } else if (w == 1) {
+        g = fe_sqr(acc.Y);
+        xput(S + 1 * 512, g, lane);
+    } else if (w == 2) {
+        sq = fe_sqr(fe_add(acc.Y, acc.Z));
+    }
+    __syncthreads();
+    if (w == 0) {
+        t = fe_mul(fe_sub(acc.X, d), fe_add(acc.X, d));
+    } else if (w == 1) {
+        xput(S + 2 * 512, fe_mul(acc.X, g), lane);  // beta
+    } else if (w == 2) {
+        g = xget(S + 1 * 512, lane);
+        d = xget(S + 0 * 512, lane);
+        xput(S + 3 * 512, fe_sqr(g), lane);                       // gamma^2
+        xput(S + 4 * 512, fe_sub(fe_sub(sq, g), d), lane);        // Z3
+    }
+    __syncthreads();
+    if (w == 0) {
+        const Fe alpha = fe_add(fe_add(t, t), t);
+        const Fe beta = xget(S + 2 * 512, lane);
+        const Fe beta2 = fe_add(beta, beta);
+        const Fe beta4 = fe_add(beta2, beta2);
+        const Fe beta8 = fe_add(beta4, beta4);
+        const Fe x3 = fe_sub(fe_sqr(alpha), beta8);
+        const Fe g2 = xget(S + 3 * 512, lane);
+        Fe g8 = fe_add(g2, g2);
+        g8 = fe_add(g8, g8);
+        g8 = fe_add(g8, g8);
+        xput(S + 5 * 512, x3, lane);
+        xput(S + 6 * 512, fe_sub(fe_mul(alpha, fe_sub(beta4, x3)), g8), lane);
+    }
+    __syncthreads();
+    acc.X = xget(S + 5 * 512, lane);
+    acc.Y = xget(S + 6 * 512, lane);
+    acc.Z = xget(S + 4 * 512, lane);
+}
+
+// acc = sel ? acc + Q : acc (add-2007-bl, Q read from the LDS table) with the field
+// multiplications spread over the four waves:
+//   L1  w0: z1z1 = Z1^2   w1: z2z2 = Z2^2   w2: zz = (Z1+Z2)^2, s2' = Y2 Z1   w3: s1' = Y1 Z2
+//   L2  w0: u2 = X2 z1z1  w1: u1 = X1 z2z2  w2: Z3' = zz - z1z1 - z2z2, s2 = s2' z1z1   w3: s1 = s1' z2z2
+//   L3  w0: h = u2 - u1, i = (2h)^2          w3: Z3 = Z3' h
+//   L4  w0: j = h i       w1: v = u1 i       w2: r = 2 (s2 - s1), r^2
+//   L5  w0: X3 = r^2 - j - 2v, r (v - X3)    w1: s1 j
+//   L6  w0: Y3 = r (v - X3) - 2 s1 j, the exceptional cases (acc or Q at infinity, acc == +-Q)
+// 5 multiplications of latency instead of 16.  Slots (512 words each): A0 B1 C2 D3 E4 F5 G6 H7 I8
+// J9 K10; the result goes to D (X), E (Y), F (Z).
+__device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool neg, int w, int lane, uint32_t *S,
+                                         const uint32_t *tab) {
+    const uint32_t *q = tab + (size_t)tab_idx * 24 * 64;
+    Jac Q;
+    Q.X = xget(q, lane);
+    Q.Y = xget(q + 8 * 64, lane);
+    Q.Z = xget(q + 16 * 64, lane);
+    if (neg) Q.Y = fe_neg(Q.Y);
+    uint32_t *A = S, *B = S + 512, *C = S + 2 * 512, *Dd = S + 3 * 512, *E = S + 4 * 512, *F = S + 5 * 512,
+             *G = S + 6 * 512, *H = S + 7 * 512, *I = S + 8 * 512, *J = S + 9 * 512, *K = S + 10 * 512;
+    Fe z1z1, z2z2, zz, s2a, s1a, u1, u2, s2, s1, h, i, j, v, x3, y3a;
+    // L1
+    if (w == 0) {
+        z1z1 = fe_sqr(acc.Z);
+        xput(A, z1z1, lane);
+    } else if (w == 1) {
+        z2z2 = fe_sqr(Q.Z);
+        xput(B, z2z2, lane);
+    } else if (w == 2) {
+        zz = fe_sqr(fe_add(acc.Z, Q.Z));
+        s2a = fe_mul(Q.Y, acc.Z);
+    } else {
+        s1a = fe_mul(acc.Y, Q.Z);
+    }
+    __syncthreads();
+    // L2
+    if (w == 0) {
+        xput(Dd, fe_mul(Q.X, z1z1), lane);  // u2
+    } else if (w == 1) {
+        u1 = fe_mul(acc.X, z2z2);
+        xput(E, u1, lane);
+    } else if (w == 2) {
+        z1z1 = xget(A, lane);
+        z2z2 = xget(B, lane);
+        xput(F, fe_sub(fe_sub(zz, z1z1), z2z2), lane);  // Z3'
+        s2 = fe_mul(s2a, z1z1);
+    } else {
+        z2z2 = xget(B, lane);
+        xput(G, fe_mul(s1a, z2z2), lane);  // s1
+    }
+    __syncthreads();
+    // L3
+    if (w == 0) {
+        u2 = xget(Dd, lane);
+        u1 = xget(E, lane);
+        h = fe_sub(u2, u1);
+        const Fe h2 = fe_add(h, h);
+        i = fe_sqr(h2);
+        xput(H, i, lane);
+    } else if (w == 3) {
+        u2 = xget(Dd, lane);
+        u1 = xget(E, lane);
+        xput(I, fe_mul(xget(F, lane), fe_sub(u2, u1)), lane);  // Z3 = Z3' h
+    }
+    __syncthreads();
+    // L4
+    if (w == 0) {
+        j = fe_mul(h, i);
+        xput(J, j, lane);
+    } else if (w == 1) {
+        i = xget(H, lane);
+        xput(K, fe_mul(u1, i), lane);  // v
+    } else if (w == 2) {
+        s1 = xget(G, lane);
+        Fe r = fe_sub(s2, s1);
+        r = fe_add(r, r);
+        xput(A, r, lane);
+        xput(B, fe_sqr(r), lane);
+    }
+    __syncthreads();
+    // L5
+    Fe r;
+    if (w == 0) {
+        v = xget(K, lane);
+        r = xget(A, lane);
+        const Fe rr = xget(B, lane);
+        x3 = fe_sub(fe_sub(rr, j), fe_add(v, v));
+        y3a = fe_mul(r, fe_sub(v, x3));
+    } else if (w == 1) {
+        s1 = xget(G, lane);
+        j = xget(J, lane);
+        xput(C, fe_mul(s1, j), lane);  // s1 j
+    }
+    __syncthreads();
+    // L6
+    if (w == 0) {
+        const Fe s1j = xget(C, lane);
+        Jac R;
+        R.X = x3;
+        R.Y = fe_sub(y3a, fe_add(s1j, s1j));
+        R.Z = xget(I, lane);
+        if (fe_is_zero(acc.Z)) {
+            R = Q;
+        } else if (fe_is_zero(Q.Z)) {
+            R = acc;
+        } else if (fe_is_zero(h)) {
+            R = fe_is_zero(r) ? jac_dbl(acc) : jac_inf();  // acc == Q / acc == -Q (rare: one lane, no barrier)
+        }
+        if (!sel) R = acc;
+        xput(Dd, R.X, lane);
+        xput(E, R.Y, lane);
+        xput(F, R.Z, lane);
+    }
+    __syncthreads();
+    acc.X = xget(Dd, lane);
+    acc.Y = xget(E, lane);
+    acc.Z = xget(F, lane);
+}
+
+__global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint8_t *__restrict__ points,
+                                                                   const uint8_t *__restrict__ scalars,
+                                                                   int per_element, int T, int D,
+                                                                   uint32_t *__restrict__ jac,
+                                                                   uint32_t *__restrict__ flags) {
+    __shared__ uint32_t S[kCoopSlots * 8 * 64];  // exchange slots, word-major: slot*512 + k*64 + lane
+    __shared__ uint32_t tab[9 * 24 * 64];        // (2t+1) P, t = 0..7: [t][24 words][64 lanes] + a spare row
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t g = (size_t)blockIdx.x * 64 + lane;
+    const bool valid = g < (size_t)T * D;
+    const int j = valid ? (int)(g / D) : 0;
+    const int i = valid ? (int)(g - (size_t)j * D) : 0;
+    // every wave loads the point and recodes the scalar itself (no exchange needed for either)
+    Jac P = jac_inf();
+    bool ok = true;
+    int8_t dig[kNafLen];
+    if (valid) {
+        ok = load_point(points + g * 64, P);
+        if (!ok) P = jac_inf();
+        wnaf5(scalars + (per_element ? g : (size_t)j) * 32, dig);
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < kNafLen; ++k) dig[k] = 0;
+    }
+    if (w == 0 && valid && !ok) atomicOr(&flags[i], 2u);
+    // table of odd multiples (2k+1) P: 2P into entry 1 as the addend, then entry k = entry k-1 + 2P
+    Jac P2 = P;
+    coop_dbl(P2, w, lane, S);
+    if (w == 0) {
+        xput(tab, P.X, lane);
+        xput(tab + 8 * 64, P.Y, lane);
+        xput(tab + 16 * 64, P.Z, lane);
+        xput(tab + 24 * 64, P2.X, lane);
+        xput(tab + 32 * 64, P2.Y, lane);
+        xput(tab + 40 * 64, P2.Z, lane);
+    }
+    __syncthreads();
+    Jac t = P;
+#pragma unroll 1
+    for (int k = 1; k < 8; ++k) {
+        coop_add(t, true, 1, false, w, lane, S, tab);   // t += 2P (entry 1 holds 2P until the end)
+        if (w == 0) {
+            uint32_t *q = tab + (size_t)(k == 1 ? 8 : k) * 24 * 64;  // (3P lands in a spare row, moved below)
+            xput(q, t.X, lane);
+            xput(q + 8 * 64, t.Y, lane);
+            xput(q + 16 * 64, t.Z, lane);
+        }
+        __syncthreads();
+    }
+    if (w == 0) {  // 3P from the spare row into entry 1
+        const uint32_t *q = tab + (size_t)8 * 24 * 64;
+        xput(tab + 24 * 64, xget(q, lane), lane);
+        xput(tab + 32 * 64, xget(q + 8 * 64, lane), lane);
+        xput(tab + 40 * 64, xget(q + 16 * 64, lane), lane);
+    }
+    __syncthreads();
+    Jac acc = jac_inf();
+#pragma unroll 1
+    for (int k = kNafLen - 1; k >= 0; --k) {
+        coop_dbl(acc, w, lane, S);  // doubling infinity keeps Z = 0: no `started` test needed
+        const int v = dig[k];
+        if (__any(v != 0)) coop_add(acc, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab);
+    }
+    if (w == 0 && valid) {
+        if (!ok) acc = jac_inf();
+        store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
+    }
+}
+
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
 // write the affine wire point and optionally SHA-256(x||y).
 // flags bit 0: base off-curve, bit 1: an input share was off-curve (ec_mul), bit 2: result at infinity.
@@ -767,8 +1028,14 @@ static void launch_ec_mul_t(const uint8_t *d_points, const uint8_t *d_scalars, i
 // threads: lanes per workgroup (64/128/256); waves: register budget, as minimum waves per SIMD
 // (2: no cap, 172 VGPRs; 4: 128 VGPRs; 8: 64 VGPRs, both with spills)
 hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
-                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves) {
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop) {
     if (T <= 0 || D <= 0) return hipSuccess;
+    if (coop) {
+        const size_t n = (size_t)T * D;
+        hipLaunchKernelGGL(ec_mul_coop_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kCoopWaves), 0, stream,
+                           d_points, d_scalars, per_element, T, D, d_jac, d_flags);
+        return hipGetLastError();
+    }
 #define FLM_EC(TPB)                                                                                          \
     switch (waves) {                                                                                         \
         case 4: launch_ec_mul_t<TPB, 4>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \

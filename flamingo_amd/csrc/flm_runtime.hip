@@ -109,6 +109,8 @@ struct flm_ctx {
     int tune_min_items = 1024;  // planner target for work items per aggregate launch (kDefaultMinItems)
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
+    int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 0: one
+                                // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
@@ -1088,6 +1090,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;
+    } else if (k == "ec_coop") {
+        if (value < -1 || value > 1) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0 or 1");
+        ctx->tune_ec_coop = value;
     } else if (k == "ec_threads") {
         if (value != 64 && value != 128 && value != 256)
             return fail(ctx, FLM_EINVAL, "ec_threads must be 64, 128 or 256");
@@ -1126,6 +1131,17 @@ static int ec_dims(flm_ctx *ctx, int T, int D) {
     return 0;
 }
 
+// Cooperative scalar multiplication (four waves, 78 KiB of LDS per 64 products: two workgroups per CU)
+// when the whole batch fits one pass of the device -- the latency-bound case, e.g. c5 seed recovery
+// (19,240 products) or one rank's pair chunk; bigger batches, and launches the caller confines to a
+// few CUs (ServerReconstruction's CU-split stream sets 0), keep one lane per product.
+int ec_coop(flm_ctx *ctx, size_t n) {
+    if (ctx->tune_ec_coop >= 0) return ctx->tune_ec_coop;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
+    return n <= (size_t)cus * 2 * 64 ? 1 : 0;
+}
+
 int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_shares, const uint8_t *d_lambdas, int T,
                        int D, int negate, uint8_t *d_points_out, uint8_t *d_seeds_out, uint32_t *d_flags,
                        void *stream) {
@@ -1138,7 +1154,7 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
-                                    ctx->tune_ec_threads, ctx->tune_ec_waves));
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D)));
     FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), T, D, negate, d_points_out, d_seeds_out,
                                        d_flags, s));
     return 0;
@@ -1261,7 +1277,7 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     FLM_HIP(ctx, hipMemsetAsync(ctx->ec_flags.p, 0, (size_t)n * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), 1, 1, n,
                                     ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s,
-                                    ctx->tune_ec_threads, ctx->tune_ec_waves));
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)n)));
     FLM_HIP(ctx, flm::launch_ec_finish(nullptr, ctx->ec_jac.as<uint32_t>(), 1, n, 0, ctx->ec_out.as<uint8_t>(),
                                        nullptr, ctx->ec_flags.as<uint32_t>(), s));
     std::vector<uint32_t> fl(n);

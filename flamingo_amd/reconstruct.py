@@ -103,6 +103,18 @@ class ServerReconstruction:
             self._bufs[name] = b
         return b
 
+    def _ec_combine(self, c1, pair_shares, lambdas, p_seeds, flags):
+        """The threshold-ElGamal combine on the side stream.  Confined to ec_cus CUs it fills them,
+        so the one-lane-per-product kernel (fewer instructions) beats the cooperative one there
+        (profiles/r02_recon_coop.log); unconfined, the library's auto choice stands."""
+        if self.ec_cus > 0:
+            self.eng.set_tuning("ec_coop", 0)
+        try:
+            self.eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
+        finally:
+            if self.ec_cus > 0:
+                self.eng.set_tuning("ec_coop", -1)
+
     def run(self, rows, L: int, lambdas, mi_shares, c1, pair_shares, pair_signs, out, stream=None,
             overlap: bool = True):
         """rows (N, pitch) int32; lambdas (T, 32), mi_shares (T, M, 32), c1 (D, 64), pair_shares
@@ -143,7 +155,7 @@ class ServerReconstruction:
         ready = torch.cuda.Event()
         ready.record(main)                       # inputs enqueued on main are visible to the side stream
         self.side.wait_event(ready)
-        eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
+        self._ec_combine(c1, pair_shares, lambdas, p_seeds, flags)
         done = torch.cuda.Event()
         done.record(self.side)
         if self.part is not None:
@@ -192,7 +204,7 @@ class ServerReconstruction:
         ready.record(caller)
         self.side.wait_event(ready)
         self.part.wait_event(ready)
-        eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
+        self._ec_combine(c1, pair_shares, lambdas, p_seeds, flags)
         side_groups = self.ec_cus * 32           # one-wave workgroups, 8 per SIMD
         side_eng.pair_units_dev(p_seeds, pair_signs, part[1], L, ws, side_groups, stream=self.side)
         done = torch.cuda.Event()

@@ -153,6 +153,11 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              scalar-multiplication kernel.
  *   "ec_waves" 1 (default: uncapped registers) | 4 | 8 minimum waves per SIMD the
  *              scalar-multiplication kernel is compiled for (more waves, more spills).
+ *   "ec_coop"  -1 (default: auto) | 0 | 1: scalar multiplications with four waves per 64 of
+ *              them, the field multiplications of each point doubling and addition spread over
+ *              the waves (a shorter latency chain for batches that leave most SIMDs idle).
+ *              Auto: cooperative when the batch fits one pass of the device (<= 128 products
+ *              per CU), else one lane per product.
  *   "small"    0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or

@@ -17,10 +17,13 @@ import ec_oracle as E
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng():
+@pytest.fixture(scope="module", params=[0, 1], ids=["per_lane", "coop"])
+def eng(request):
+    """Every test runs with both scalar-multiplication kernels: one lane per product
+    (ec_mul_kernel) and four cooperating waves per 64 products (ec_mul_coop_kernel)."""
     from flamingo_amd import MaskEngine
     e = MaskEngine(0)
+    e.set_tuning("ec_coop", request.param)
     yield e
     e.close()
 

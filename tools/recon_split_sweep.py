@@ -38,6 +38,7 @@ cases = [(c, f, tn) for tn in tunes for c, f in cases]
 for ec_cus, f, (ec_threads, ec_waves) in cases:
     eng.set_tuning("ec_threads", ec_threads)
     eng.set_tuning("ec_waves", ec_waves)
+    eng.set_tuning("ec_coop", int(os.environ.get("EC_COOP", "0")))
     q = f == "q"
     rec = ServerReconstruction(eng, pass1_min_items=int(os.environ.get("MIN_ITEMS", "4096")), ec_cus=ec_cus, cu_pick=os.environ.get("CU_PICK", "first"),
                                pair_split=0.0 if q else float(f), pair_queue=q)
@@ -53,4 +54,4 @@ for ec_cus, f, (ec_threads, ec_waves) in cases:
     torch.cuda.synchronize()
     ok = bool(torch.all(out == len(on)).item())
     rec.close()
-    print(f"ec_cus={ec_cus} ec_threads={ec_threads} ec_waves={ec_waves} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
+    print(f"ec_coop={os.environ.get('EC_COOP', '0')} ec_cus={ec_cus} ec_threads={ec_threads} ec_waves={ec_waves} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
