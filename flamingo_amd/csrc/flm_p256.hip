@@ -624,14 +624,19 @@ __global__ __launch_bounds__(TPB, WPE) void ec_mul_kernel(const uint8_t *__restr
 constexpr int kCoopWaves = 4;
 constexpr int kCoopSlots = 11;
 
+// lane-major slots: a lane's 8 words are 32 contiguous bytes, moved with two 16-byte LDS ops
+// (0.5-1 % faster than word-major single-dword ops, profiles/r02_ab_coop_b128.log)
 __device__ __forceinline__ void xput(uint32_t *slot, const Fe &a, int lane) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) slot[k * 64 + lane] = a.v[k];
+    uint4 *q = reinterpret_cast<uint4 *>(slot + lane * 8);
+    q[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    q[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
 }
 __device__ __forceinline__ Fe xget(const uint32_t *slot, int lane) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(slot + lane * 8);
+    const uint4 x = q[0], y = q[1];
     Fe a;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a.v[k] = slot[k * 64 + lane];
+    a.v[0] = x.x; a.v[1] = x.y; a.v[2] = x.z; a.v[3] = x.w;
+    a.v[4] = y.x; a.v[5] = y.y; a.v[6] = y.z; a.v[7] = y.w;
     return a;
 }
 
@@ -803,8 +808,8 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
                                                                    int per_element, int T, int D,
                                                                    uint32_t *__restrict__ jac,
                                                                    uint32_t *__restrict__ flags) {
-    __shared__ uint32_t S[kCoopSlots * 8 * 64];  // exchange slots, word-major: slot*512 + k*64 + lane
-    __shared__ uint32_t tab[9 * 24 * 64];        // (2t+1) P, t = 0..7: [t][24 words][64 lanes] + a spare row
+    __shared__ __attribute__((aligned(16))) uint32_t S[kCoopSlots * 8 * 64];  // exchange slots, 512 words each
+    __shared__ __attribute__((aligned(16))) uint32_t tab[9 * 24 * 64];  // (2t+1) P, t = 0..7, + a spare row
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const size_t g = (size_t)blockIdx.x * 64 + lane;
