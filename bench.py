@@ -293,8 +293,9 @@ RECON_EC_FRAC = 24 / 256  # share of the CUs given to the EC combine in the CU-s
 RECON_MIN_ITEMS = 4096   # unmask items of the CU-split schedule's first pass
 RECON_QUEUE_MIN_ITEMS = 4096  # its pass 1 plan: 4 same-tile row/seed parts per tile (merged kernel, atomics):
                              # 8.17 ms vs 8.28 at 1024 items (profiles/r02_recon_minitems.log)
-RECON_QUEUE_EC_FRAC = 32 / 256  # EC CUs of the pair-queue schedule (recon_split_sweep: 16 / 24 / 32 / 40 / 48 CUs ->
-                                # 11.0 / 9.52 / 8.65 / 9.28 / 9.52 ms at c5; profiles/r02_recon_sweep.log)
+RECON_QUEUE_EC_FRAC = 24 / 256  # EC CUs of the pair-queue schedule, with RECON_QUEUE_EC_TERMS combine terms per lane
+RECON_QUEUE_EC_TERMS = 2        # (Straus): 16 / 24 / 32 CUs -> 9.78 / 8.05 / 8.28 ms; one term per lane on 32 CUs
+                                # 8.46 (profiles/r02_straus_recon.log, r02_recon_sweep.log)
 
 
 def settle_clock(torch, step, stream, ms, agree=None):
@@ -353,7 +354,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         q_cus = max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count() / 8)) * 8) if eng.cu_count() >= 64 else \
             max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count())))
         recon_q = ServerReconstruction(eng, dev, pass1_min_items=RECON_QUEUE_MIN_ITEMS, ec_cus=q_cus,
-                                       cu_pick="first", pair_queue=True)
+                                       cu_pick="first", pair_queue=True, ec_terms=RECON_QUEUE_EC_TERMS)
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         n_off = int(round(dropout * N))
@@ -447,7 +448,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
                         "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
                         f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS}); "
-                        f"cu_split_queue: EC on {recon_q.ec_cus} CUs, which then claim pair-mask units from a "
+                        f"cu_split_queue: EC on {recon_q.ec_cus} CUs ({recon_q.ec_terms} combine terms per lane), which then claim pair-mask units from a "
                         "device work queue until the self-mask pass ends; the last pass takes the rest on all CUs"}
         recon_cu.close()
         recon_q.close()

@@ -607,6 +607,62 @@ __global__ __launch_bounds__(TPB, WPE) void ec_mul_kernel(const uint8_t *__restr
     store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
 }
 
+// ------------------------------------------------ Straus: NT terms per lane
+// The combine's sum_j lambda_j share_{j,i} with NT consecutive terms per lane sharing ONE chain
+// of doublings (Straus / Shamir's trick): ~256 doublings + NT x ~43 additions + NT tables per lane
+// instead of NT x (256 + 43 + 8) -- 35 % less work at NT = 2, for a longer chain per lane.  Worth it
+// where the combine is throughput-bound (ServerReconstruction's 32 EC CUs).  Output: the per-lane
+// partial sums as SoA planes [ceil(T/NT)][24][D] for ec_finish_kernel.  Off-curve points count as
+// infinity and set flag bit 1, as in ec_mul_kernel.
+template <int NT>
+__global__ __launch_bounds__(kEcThreads) void ec_mul_straus_kernel(const uint8_t *__restrict__ points,
+                                                                  const uint8_t *__restrict__ scalars, int T, int D,
+                                                                  uint32_t *__restrict__ jac,
+                                                                  uint32_t *__restrict__ flags) {
+    __builtin_amdgcn_s_setprio(3);
+    const int Tg = (T + NT - 1) / NT;
+    const size_t g = (size_t)blockIdx.x * kEcThreads + threadIdx.x;
+    if (g >= (size_t)Tg * D) return;
+    const int jg = (int)(g / D);
+    const int i = (int)(g - (size_t)jg * D);
+    int8_t dig[NT][kNafLen];
+    Jac tab[NT][8];
+#pragma unroll 1
+    for (int u = 0; u < NT; ++u) {
+        const int j = jg * NT + u;
+        Jac P = jac_inf();
+        if (j < T) {
+            if (!load_point(points + ((size_t)j * D + i) * 64, P)) {
+                atomicOr(&flags[i], 2u);
+                P = jac_inf();
+            }
+            wnaf5(scalars + (size_t)j * 32, dig[u]);
+        } else {
+#pragma unroll 1
+            for (int k = 0; k < kNafLen; ++k) dig[u][k] = 0;
+        }
+        tab[u][0] = P;
+        const Jac P2 = jac_dbl(P);
+#pragma unroll 1
+        for (int t = 1; t < 8; ++t) tab[u][t] = jac_add(tab[u][t - 1], P2);
+    }
+    Jac acc = jac_inf();
+#pragma unroll 1
+    for (int w = kNafLen - 1; w >= 0; --w) {
+        acc = jac_dbl(acc);  // doubling infinity keeps Z = 0
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+            const int v = dig[u][w];
+            if (v) {
+                Jac Q = tab[u][(v < 0 ? -v : v) >> 1];
+                if (v < 0) Q.Y = fe_neg(Q.Y);
+                acc = jac_add(acc, Q);
+            }
+        }
+    }
+    store_jac(jac + (size_t)jg * 24 * D + i, (size_t)D, acc);
+}
+
 // ------------------------------------------------ cooperative scalar multiplication
 // The same product as ec_mul_kernel, with FOUR waves (on the CU's four SIMDs) per 64 scalar
 // multiplications: lane l of every wave works on item g = blockIdx.x * 64 + l, and the field
@@ -1032,9 +1088,25 @@ static void launch_ec_mul_t(const uint8_t *d_points, const uint8_t *d_scalars, i
 
 // threads: lanes per workgroup (64/128/256); waves: register budget, as minimum waves per SIMD
 // (2: no cap, 172 VGPRs; 4: 128 VGPRs; 8: 64 VGPRs, both with spills)
+int ec_mul_groups(int T, int terms) { return terms > 1 ? (T + terms - 1) / terms : T; }
+
 hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
-                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop) {
+                         uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop,
+                         int terms) {
     if (T <= 0 || D <= 0) return hipSuccess;
+    if (terms > 1 && !per_element) {
+        const size_t n = (size_t)ec_mul_groups(T, terms) * D;
+        const dim3 grid((unsigned)((n + kEcThreads - 1) / kEcThreads));
+        if (terms == 2)
+            hipLaunchKernelGGL(ec_mul_straus_kernel<2>, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, T, D,
+                               d_jac, d_flags);
+        else if (terms == 4)
+            hipLaunchKernelGGL(ec_mul_straus_kernel<4>, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, T, D,
+                               d_jac, d_flags);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     if (coop) {
         const size_t n = (size_t)T * D;
         hipLaunchKernelGGL(ec_mul_coop_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kCoopWaves), 0, stream,

@@ -109,6 +109,7 @@ struct flm_ctx {
     int tune_min_items = 1024;  // planner target for work items per aggregate launch (kDefaultMinItems)
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
+    int tune_ec_terms = 1;      // combine terms per lane (1, 2, 4: Straus, shared doublings)
     int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
@@ -1090,6 +1091,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;
+    } else if (k == "ec_terms") {
+        if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_terms must be 1, 2 or 4");
+        ctx->tune_ec_terms = value;
     } else if (k == "ec_coop") {
         if (value < -1 || value > 1) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0 or 1");
         ctx->tune_ec_coop = value;
@@ -1153,9 +1157,11 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
+    const int terms = ec_coop(ctx, (size_t)T * D) ? 1 : ctx->tune_ec_terms;
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
-                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D)));
-    FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), T, D, negate, d_points_out, d_seeds_out,
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D), terms));
+    FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), flm::ec_mul_groups(T, terms), D, negate,
+                                       d_points_out, d_seeds_out,
                                        d_flags, s));
     return 0;
 }

@@ -52,8 +52,11 @@ import torch
 
 class ServerReconstruction:
     def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride",
-                 pair_split: float = 0.0, pair_queue: bool = False):
+                 pair_split: float = 0.0, pair_queue: bool = False, ec_terms: int = 1):
         self.eng = engine
+        if ec_terms not in (1, 2, 4):
+            raise ValueError("ec_terms must be 1, 2 or 4")
+        self.ec_terms = int(ec_terms)
         self.pass1_min_items = pass1_min_items
         if not 0.0 <= pair_split < 1.0:
             raise ValueError("pair_split must be in [0, 1)")
@@ -106,14 +109,18 @@ class ServerReconstruction:
     def _ec_combine(self, c1, pair_shares, lambdas, p_seeds, flags):
         """The threshold-ElGamal combine on the side stream.  Confined to ec_cus CUs it fills them,
         so the one-lane-per-product kernel (fewer instructions) beats the cooperative one there
-        (profiles/r02_recon_coop.log); unconfined, the library's auto choice stands."""
+        (profiles/r02_recon_coop.log), and `ec_terms` products per lane share one chain of
+        doublings (Straus: 2 terms on 24 CUs 8.05 ms vs 1 term on 32 CUs 8.46, profiles/r02_straus_recon.log);
+        unconfined, the library's auto choice stands."""
         if self.ec_cus > 0:
             self.eng.set_tuning("ec_coop", 0)
+            self.eng.set_tuning("ec_terms", self.ec_terms)
         try:
             self.eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
         finally:
             if self.ec_cus > 0:
                 self.eng.set_tuning("ec_coop", -1)
+                self.eng.set_tuning("ec_terms", 1)
 
     def run(self, rows, L: int, lambdas, mi_shares, c1, pair_shares, pair_signs, out, stream=None,
             overlap: bool = True):

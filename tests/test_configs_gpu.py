@@ -5,7 +5,7 @@ c3: n=1024 clients, L=2^18, neighbourhood -o 2 (config/flamingo.py:37-38), the r
     server round; out == |U| everywhere, and three slot windows against the oracle bit for bit.
 c5: n=4096, L=2^20, 1 % dropouts, two iterations: the server gets m_i and s_ij only as Shamir /
     threshold-ElGamal decryption shares (flamingo_amd.synthetic) and ServerReconstruction
-    (pair-queue schedule, the bench's fastest) recovers them and unmasks on the GPU; out == |U|
+    (pair-queue schedule on 24 EC CUs with two combine terms per lane, the bench's) recovers them and unmasks on the GPU; out == |U|
     everywhere and windows against the oracle, which is given the recovered seeds' expected
     values (the round's own server seed table).
 """
@@ -71,7 +71,7 @@ def test_c5_full_size_reconstruction(eng):
     m = np.frombuffer(b"".join(P.bench_seed("c5", i) for i in range(N)), np.uint8).reshape(N, 32)
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
-    rec = ServerReconstruction(eng, ec_cus=32, cu_pick="first", pass1_min_items=1024, pair_queue=True)
+    rec = ServerReconstruction(eng, ec_cus=24, cu_pick="first", pass1_min_items=4096, pair_queue=True, ec_terms=2)
     cache = {}
     try:
         for it in (1, 2):

@@ -17,13 +17,16 @@ import ec_oracle as E
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[0, 1], ids=["per_lane", "coop"])
+@pytest.fixture(scope="module", params=[(0, 1), (1, 1), (0, 2), (0, 4)],
+                ids=["per_lane", "coop", "straus2", "straus4"])
 def eng(request):
-    """Every test runs with both scalar-multiplication kernels: one lane per product
-    (ec_mul_kernel) and four cooperating waves per 64 products (ec_mul_coop_kernel)."""
+    """Every test runs with each scalar-multiplication kernel: one lane per product (ec_mul_kernel),
+    four cooperating waves per 64 products (ec_mul_coop_kernel), and 2 / 4 combine terms per lane
+    sharing one chain of doublings (ec_mul_straus_kernel; the combine only)."""
     from flamingo_amd import MaskEngine
     e = MaskEngine(0)
-    e.set_tuning("ec_coop", request.param)
+    e.set_tuning("ec_coop", request.param[0])
+    e.set_tuning("ec_terms", request.param[1])
     yield e
     e.close()
 

@@ -46,7 +46,10 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
     pair_split = ServerReconstruction(eng, ec_cus=32, cu_pick="first", pass1_min_items=4096, pair_split=0.4)
     # CU-partitioned, the EC CUs claim pair-mask units from a queue until the self-mask pass ends
     queue = ServerReconstruction(eng, ec_cus=32, pass1_min_items=4096, pair_queue=True)
-    for overlap, rec in ((True, rec), (False, rec), (True, split), (True, pair_split), (True, queue)):
+    # the bench's schedule: the queue on 24 EC CUs with two combine terms per lane (Straus)
+    queue2 = ServerReconstruction(eng, ec_cus=24, cu_pick="first", pass1_min_items=4096, pair_queue=True, ec_terms=2)
+    for overlap, rec in ((True, rec), (False, rec), (True, split), (True, pair_split), (True, queue),
+                         (True, queue2)):
         out = torch.empty(L, dtype=torch.int32, device=dev)
         _, flags = rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out,
                            overlap=overlap)
@@ -59,6 +62,7 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
     split.close()
     pair_split.close()
     queue.close()
+    queue2.close()
     if n_off:
         assert R["D"] > 0
 

@@ -26,6 +26,7 @@ ap.add_argument("--cpu-sample", type=int, default=100, help="scalar mults timed 
 ap.add_argument("--threads", type=int, default=64)
 ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
+ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
 ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
 a = ap.parse_args()
 
@@ -42,6 +43,7 @@ dev = torch.device("cuda:0")
 eng = MaskEngine(0)
 eng.set_tuning("ec_threads", a.threads)
 eng.set_tuning("ec_coop", a.coop)
+eng.set_tuning("ec_terms", a.terms)
 c1_t = torch.from_numpy(c1).to(dev)
 sh_t = torch.from_numpy(shares).to(dev)
 lam_t = torch.from_numpy(C.scalars_to_wire(lams)).to(dev)
@@ -75,7 +77,7 @@ t = time.perf_counter()
 for i in range(a.cpu_sample):
     C.mul(lams[i % a.T], base[i % 64])
 cpu_per_mul = (time.perf_counter() - t) / a.cpu_sample
-print(json.dumps({"lib": os.environ.get("FLM_LIB_PATH", "default"), "coop": a.coop, "cus": a.cus, "threads": a.threads, "D": a.D, "T": a.T, "scalars": a.scalars, "lambda_hex": [hex(x)[:12] for x in lams[:4]], "gpu_ms": round(gpu_ms, 4),
+print(json.dumps({"lib": os.environ.get("FLM_LIB_PATH", "default"), "coop": a.coop, "terms": a.terms, "cus": a.cus, "threads": a.threads, "D": a.D, "T": a.T, "scalars": a.scalars, "lambda_hex": [hex(x)[:12] for x in lams[:4]], "gpu_ms": round(gpu_ms, 4),
                   "gpu_scalar_mults_per_s": round(a.D * a.T / gpu_ms * 1e3),
                   "cpu_openssl_ms_est": round(cpu_per_mul * a.D * a.T * 1e3, 1),
                   "cpu_openssl_us_per_mul": round(cpu_per_mul * 1e6, 1), "cpu_cores": 1}))

@@ -39,6 +39,7 @@ for ec_cus, f, (ec_threads, ec_waves) in cases:
     eng.set_tuning("ec_threads", ec_threads)
     eng.set_tuning("ec_waves", ec_waves)
     eng.set_tuning("ec_coop", int(os.environ.get("EC_COOP", "0")))
+    eng.set_tuning("ec_terms", int(os.environ.get("EC_TERMS", "1")))
     q = f == "q"
     rec = ServerReconstruction(eng, pass1_min_items=int(os.environ.get("MIN_ITEMS", "4096")), ec_cus=ec_cus, cu_pick=os.environ.get("CU_PICK", "first"),
                                pair_split=0.0 if q else float(f), pair_queue=q)
@@ -54,4 +55,4 @@ for ec_cus, f, (ec_threads, ec_waves) in cases:
     torch.cuda.synchronize()
     ok = bool(torch.all(out == len(on)).item())
     rec.close()
-    print(f"ec_coop={os.environ.get('EC_COOP', '0')} ec_cus={ec_cus} ec_threads={ec_threads} ec_waves={ec_waves} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
+    print(f"ec_coop={os.environ.get('EC_COOP', '0')} ec_terms={os.environ.get('EC_TERMS', '1')} ec_cus={ec_cus} ec_threads={ec_threads} ec_waves={ec_waves} pair_split={f} ms={e0.elapsed_time(e1) / 6:.3f} correct={ok}", flush=True)
