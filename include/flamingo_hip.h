@@ -158,7 +158,10 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              the waves (a shorter latency chain for batches that leave most SIMDs idle).
  *              Auto: cooperative when the batch fits one pass of the device (<= 128 products
  *              per CU), else one lane per product.
- *   "small"    0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
+ *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
+ *              (Straus: the terms share one chain of doublings); ignored when the combine
+ *              runs cooperatively.
+ *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or
  *              mask_hi == L).  That path builds no device seed table: a following
