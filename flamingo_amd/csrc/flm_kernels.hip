@@ -291,6 +291,25 @@ __device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32
 }
 
 // --------------------------------------------------------------- main kernel
+#ifdef FLM_STATIC_UNITS
+constexpr bool kClaimUnits = false;  // probe build: the static split of rows and seeds over the waves
+#else
+constexpr bool kClaimUnits = true;
+#endif
+#ifdef FLM_WG_TRACE
+// probe build only: per workgroup of items_kernel, [start, seeds done, end] in s_memrealtime ticks
+// (100 MHz) and the hardware ids (HW_ID | XCC_ID << 32), read back by flm_debug_wg_trace
+__device__ uint64_t flm_wg_trace[4 * 65536];
+#define FLM_WG_MARK(slot)                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {                                                  \
+        flm_wg_trace[4 * blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime();                  \
+        if ((slot) == 0)                                                                           \
+            flm_wg_trace[4 * blockIdx.x + 3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) |       \
+                                               ((uint64_t)__builtin_amdgcn_s_getreg(0x7814) << 32); \
+    }
+#else
+#define FLM_WG_MARK(slot)
+#endif
 // One workgroup = one Item.  Wave w works on sub-tile s = w % S with chunk
 // c = w / S of the item's rows and seeds (Cw = 16 / S chunks).
 //   BL      rows are loaded in block layout (lane t: slots 16t..16t+15), the
@@ -310,11 +329,17 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
     constexpr int Cw = kWavesPerGroup / S;
     constexpr int RU = MERGED ? RUM : 4;  // rows in flight per wave in the rows-only loop
     __shared__ u32x4 lds[kWavesPerGroup * 256];  // 64 KiB: one 4 KiB region per wave
+    __shared__ uint32_t claim[S];                 // next unclaimed unit of each sub-tile
 
+    FLM_WG_MARK(0);
     const Item it = items[blockIdx.x];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int s = w % S, c = w / S;
+    if constexpr (kClaimUnits && !SPREAD && Cw > 1) {
+        if (threadIdx.x < S) claim[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     const uint32_t flags = it.flags;
     const bool has_rows = flags & kHasRows, has_mask = flags & kHasMask;
 
@@ -375,6 +400,61 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
             chacha_mask_add(rec, ctr, m);
             ++rec;
         }
+    } else if constexpr (kClaimUnits && Cw > 1) {
+        // Units claimed from a per-sub-tile LDS counter: unit i = seed i of the item, plus row i
+        // when there is one.  With a static split (64 seeds per wave at c4) the SIMD's arbiter
+        // lets some waves run far ahead, and a workgroup waited at its barrier for its slowest
+        // wave: 0.33-0.62 ms workgroup times, wave 0 idle ~0.2 ms of them, 87 % mean residency
+        // (tools/wg_trace.py, profiles/r02_wg_trace.log).  Claiming, a fast wave takes more
+        // units and the waves of a workgroup finish within about one block of each other.
+        // Any split gives the same bits: the partials are summed mod 2^32.
+        const uint32_t NR = (has_rows && row_valid > 0) ? it.nrows : 0u;
+        const uint32_t NS = has_mask ? it.nseeds : 0u;
+        const uint32_t *rb = rows + it.row_in + sub_slot;
+        for (;;) {
+            uint32_t v = 0;
+            if (lane == 0) v = __hip_atomic_fetch_add(&claim[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t i = __builtin_amdgcn_readlane(v, 0);
+            if (i >= NS) break;
+#ifdef FLM_CLAIM_PRIO
+            {   // probe: the further a workgroup has got, the lower its waves' issue priority
+                const uint32_t q4 = (uint32_t)(((uint64_t)i * 4u) / NS);
+                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
+                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
+                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
+            if (i < NR) {
+                u32x4 v4[4];
+                load_row<BL, AUX>(rb + (uint64_t)i * row_pitch, row_bytes, lane, v4);
+                chacha_mask_add(recs + it.k0 + i, ctr, m);
+                add_row(v4);
+            } else {
+                chacha_mask_add(recs + it.k0 + i, ctr, m);
+            }
+        }
+        // rows past the last seed (seed-light items): the static split, RU rows in flight
+        if (NR > NS) {
+            const uint32_t a = NS + (uint32_t)(((uint64_t)(NR - NS) * c) / Cw);
+            const uint32_t b = NS + (uint32_t)(((uint64_t)(NR - NS) * (c + 1)) / Cw);
+            const uint32_t *rq = rb + (uint64_t)a * row_pitch;
+            uint32_t rr = b - a;
+            for (; rr >= RU; rr -= RU) {
+                u32x4 v4[RU][4];
+#pragma unroll
+                for (int u = 0; u < RU; ++u) load_row<BL, AUX>(rq + u * row_pitch, row_bytes, lane, v4[u]);
+#pragma unroll
+                for (int u = 0; u < RU; ++u) add_row(v4[u]);
+                rq += RU * row_pitch;
+            }
+            for (; rr > 0; --rr) {
+                u32x4 v4[4];
+                load_row<BL, AUX>(rq, row_bytes, lane, v4);
+                add_row(v4);
+                rq += row_pitch;
+            }
+        }
     } else {
         // paired phase: one row load in flight under one ChaCha block per step
         const uint32_t np = nr < ns ? nr : ns;
@@ -409,6 +489,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         }
     }
 
+    FLM_WG_MARK(1);
     // ---- combine through this wave's LDS region (natural slot order), then
     // sum the Cw chunk partials of every sub-tile and write the tile.
     u32x4 *R = lds + w * 256;
@@ -423,6 +504,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         const int valid = has_mask ? (int)it.mask_valid : (int)it.row_valid;
         const uint32_t bias = (has_rows ? it.row_bias : 0u) + (has_mask ? mbias : 0u);
         reduce_out<S>(lds, out, base, valid, bias, (flags & (kRowAtomic | kMaskAtomic)) != 0);
+        FLM_WG_MARK(2);
     } else {
         const bool same = flags & kSameTile;
         u32x4 mq[4];
@@ -937,3 +1019,10 @@ hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], u
 }
 
 }  // namespace flm
+
+#ifdef FLM_WG_TRACE
+extern "C" int flm_debug_wg_trace(uint64_t *host, int n_items) {
+    const size_t n = (size_t)(n_items < 65536 ? n_items : 65536) * 4 * sizeof(uint64_t);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(flm::flm_wg_trace), n, 0, hipMemcpyDeviceToHost);
+}
+#endif
