@@ -5,7 +5,7 @@ and after the store, plus XCC / CU ids.  Prints the launch span, the start/end s
 workgroup generations, and the mean workgroup residency over the span (slots = 2 per CU).
 
 usage: FLM_LIB_PATH=.../libflamingo_hip.so wg_trace.py MODE [--subtiles S] [--min-items M]
-  MODE = mask | full (the c4 launch shapes of tools/clock_probe.py)"""
+  MODE = mask | full (the c4 launch shapes of tools/clock_probe.py) | c3 (N=K=1024, L=2^18)"""
 import argparse
 import ctypes
 import json
@@ -21,18 +21,18 @@ from flamingo_amd import MaskEngine  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=("mask", "full"))
+    ap.add_argument("mode", choices=("mask", "full", "c3"))
     ap.add_argument("--subtiles", type=int, default=0)
     ap.add_argument("--min-items", type=int, default=1024)
     ap.add_argument("--settle-ms", type=float, default=200.0)
     a = ap.parse_args()
-    N, K, L = 1024, 1024, 1 << 20
+    N, K, L = 1024, 1024, (1 << 18) if a.mode == "c3" else (1 << 20)
     eng = MaskEngine(0)
     eng.set_tuning("subtiles", a.subtiles)
     eng.set_tuning("min_items", a.min_items)
     g = torch.Generator(device="cuda").manual_seed(1)
     rows = torch.randint(-2**31, 2**31 - 1, (N, L), dtype=torch.int32, device="cuda", generator=g) \
-        if a.mode == "full" else None
+        if a.mode in ("full", "c3") else None
     seeds = torch.randint(0, 256, (K, 32), dtype=torch.uint8, device="cuda", generator=g)
     signs = torch.full((K,), -1, dtype=torch.int8, device="cuda")
     out = torch.empty(L, dtype=torch.int32, device="cuda")
@@ -67,6 +67,8 @@ def main():
         # generation: a workgroup whose start is after the earliest end began in the second wave
         gen2 = start > np.sort(end)[0] * 0.5
         slots = 2 * 256
+        if os.environ.get("WG_TRACE_DUMP"):
+            np.save(os.environ["WG_TRACE_DUMP"] + f".{rep}.npy", buf)
         busy = dur.sum() / (slots * span)
         r = {"mode": a.mode, "subtiles": a.subtiles, "items": int(n), "span_us": round(span / 1e3, 1),
              "wg_us_p0_p50_p100": [round(float(np.percentile(dur, q)) / 1e3, 1) for q in (0, 50, 100)],
@@ -85,8 +87,6 @@ def main():
              "distinct_cu": int(len(set(zip(xcc.tolist(), se.tolist(), sh.tolist(), cu.tolist()))))}
         res.append(r)
         print(json.dumps(r), flush=True)
-    if os.environ.get("WG_TRACE_DUMP"):
-        np.save(os.environ["WG_TRACE_DUMP"], buf)
 
 
 if __name__ == "__main__":
