@@ -411,29 +411,26 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         const uint32_t NR = (has_rows && row_valid > 0) ? it.nrows : 0u;
         const uint32_t NS = has_mask ? it.nseeds : 0u;
         const uint32_t *rb = rows + it.row_in + sub_slot;
-        for (;;) {
+        // one lane adds 1 to the counter; in asm so that the compiler's atomic optimizer does not
+        // wrap it in a wave reduction (mbcnt/bcnt/readfirstlane: ~8 VALU per unit)
+        const uint32_t caddr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&claim[s];
+        auto next = [&]() -> uint32_t {
             uint32_t v = 0;
-            if (lane == 0) v = __hip_atomic_fetch_add(&claim[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t i = __builtin_amdgcn_readlane(v, 0);
-            if (i >= NS) break;
-#ifdef FLM_CLAIM_PRIO
-            {   // probe: the further a workgroup has got, the lower its waves' issue priority
-                const uint32_t q4 = (uint32_t)(((uint64_t)i * 4u) / NS);
-                if (q4 == 0) __builtin_amdgcn_s_setprio(3);
-                else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
-                else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
-                else __builtin_amdgcn_s_setprio(0);
-            }
-#endif
-            if (i < NR) {
-                u32x4 v4[4];
-                load_row<BL, AUX>(rb + (uint64_t)i * row_pitch, row_bytes, lane, v4);
-                chacha_mask_add(recs + it.k0 + i, ctr, m);
-                add_row(v4);
-            } else {
-                chacha_mask_add(recs + it.k0 + i, ctr, m);
-            }
+            if (lane == 0)
+                asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(caddr), "v"(1u) : "memory");
+            return __builtin_amdgcn_readlane(v, 0);
+        };
+        // two loops, one body each: a single loop with a row / no-row branch made the compiler
+        // copy the 16 accumulators at every unit
+        const uint32_t NP = NR < NS ? NR : NS;
+        uint32_t i = next();
+        for (; i < NP; i = next()) {
+            u32x4 v4[4];
+            load_row<BL, AUX>(rb + (uint64_t)i * row_pitch, row_bytes, lane, v4);
+            chacha_mask_add(recs + it.k0 + i, ctr, m);
+            add_row(v4);
         }
+        for (; i < NS; i = next()) chacha_mask_add(recs + it.k0 + i, ctr, m);
         // rows past the last seed (seed-light items): the static split, RU rows in flight
         if (NR > NS) {
             const uint32_t a = NS + (uint32_t)(((uint64_t)(NR - NS) * c) / Cw);
