@@ -44,7 +44,7 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 G
 # clock for the c4 and the mask-only launch.
 PROBE_CHACHA_CEILING_GWORDS = 733.0
 CPI_SUMMARY = "profiles/r02_clock_cpi_summary.json"
-CHACHA_OPS_PER_WORD = 61.3       # VALU instructions per mask word in items_kernel (PMC: 1.028e9 wave-instructions x 64 / 2^30 words, profiles/r02_profile_summary.json)
+CHACHA_OPS_PER_WORD = 61.5       # VALU instructions per mask word in items_kernel (PMC: 1.031e9 wave-instructions x 64 / 2^30 words, profiles/r02_profile_summary.json)
 
 
 def parse():
