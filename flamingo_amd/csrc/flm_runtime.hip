@@ -296,6 +296,7 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
 constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this many a whole-vector round is not split
 constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
+constexpr int kWindowItems = 512;         // item target of a windowed (slot-sharded) round: 2 per CU
 
 // Host-only planning of one aggregate round (no device state): fills `items`
 // and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
@@ -307,7 +308,12 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     // row-streaming-heavy rounds (few seeds per slot) prefer 4 sub-tiles per
     // workgroup: 4096-slot tiles, fewer LDS combines (measured 5.77 vs 5.26 TB/s).
     const bool seed_light = (uint64_t)K * (mask_hi - mask_lo) * 2 < (uint64_t)N * L;
-    const int subtiles = tune_subtiles > 0 ? tune_subtiles : (seed_light ? 4 : 1);
+    // A rank of the slot-sharded round (rows over all of L, masks over a window): 4096-slot
+    // tiles and kWindowItems items, one generation of workgroups on the chip.  One rank of the
+    // strong-scaled c4 round, G = 8: 0.179 -> 0.169 ms; G = 4: 0.364 -> 0.350-0.360 ms; G = 2 the
+    // same (profiles/r02_ab_strong_plan.log).
+    const bool windowed = N > 0 && K > 0 && (mask_lo > 0 || mask_hi < L);
+    const int subtiles = tune_subtiles > 0 ? tune_subtiles : ((seed_light || windowed) ? 4 : 1);
     const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
     Job j;
     j.nrows = (uint32_t)N;
@@ -332,7 +338,9 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
                (uint64_t)pr * 2 * 16 <= (uint64_t)K)
             pr = pm = pr * 2;
     } else {
-        choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)min_items);
+        const int target = (windowed && !seed_light && tune_subtiles <= 0 && min_items == kDefaultMinItems)
+                               ? kWindowItems : min_items;
+        choose_parts(tr, tm, (uint32_t)N, (uint32_t)K, pr, pm, (uint64_t)target);
     }
     plan.subtiles = subtiles;
     plan.seed_light = seed_light;

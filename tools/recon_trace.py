@@ -32,7 +32,8 @@ t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
 QUEUE = os.environ.get("QUEUE", "0") == "1"
-rec = ServerReconstruction(eng, pass1_min_items=MIN_ITEMS, ec_cus=EC_CUS, cu_pick="first", pair_queue=QUEUE)
+rec = ServerReconstruction(eng, pass1_min_items=MIN_ITEMS, ec_cus=EC_CUS, cu_pick="first", pair_queue=QUEUE,
+                           ec_terms=int(os.environ.get("EC_TERMS", "1")))
 with torch.cuda.stream(main):
     for _ in range(4):
         rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out, stream=main)
