@@ -5,7 +5,7 @@ OUT=$1; N=$2; shift 2
 R=$(pwd)
 : > $OUT
 for i in $(seq $N); do
-  for CU in 0 32; do
+  for CU in ${EC_AB_CUS:-0 32}; do
     for V in "$@"; do
       export FLM_LIB_PATH=$R/flamingo_amd/lib_v/$V/libflamingo_hip.so
       echo -n "$V " >> $OUT
