@@ -44,6 +44,8 @@ for ec_cus, f, (ec_threads, ec_waves) in cases:
     rec = ServerReconstruction(eng, pass1_min_items=int(os.environ.get("MIN_ITEMS", "4096")), ec_cus=ec_cus, cu_pick=os.environ.get("CU_PICK", "first"),
                                pair_split=0.0 if q else float(f), pair_queue=q,
                                ec_terms=int(os.environ.get("EC_TERMS", "1")))
+    if os.environ.get("PASS1_ALL") == "1":
+        rec.part = torch.cuda.Stream()   # probe: pass 1 on every CU, the EC still confined to its CUs
     args = (r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out)
     with torch.cuda.stream(main):
         for _ in range(2):
