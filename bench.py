@@ -625,7 +625,9 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
             "correct": bool(okt.item()),
             "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
                         "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "
-                        "shard; reduce-scatter (library RCCL communicator, ncclUint32)"}
+                        "shard; reduce-scatter ("
+                        + ("library RCCL communicator, ncclUint32" if backend == "nccl" else f"torch.distributed {backend}")
+                        + ")"}
 
 
 def committed_cpi():

@@ -1,5 +1,5 @@
 #!/bin/bash
-# bench.py's weak-scaled G=4 round on a one-GPU box (four ranks share the GPU; the reduce-scatter
+# bench.py's G=4 round (default: c4 strong plus the sharded c5) on a one-GPU box (four ranks share the GPU; the reduce-scatter
 # runs over gloo on host copies because RCCL refuses duplicate devices).  Full c4 sizes per rank:
 # checks the G=4 window planning and the out == |U| invariant across ranks, not the timing.
 mkdir -p gpurun_out

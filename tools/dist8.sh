@@ -1,5 +1,5 @@
 #!/bin/bash
-# bench.py's weak-scaled G=8 round on a one-GPU box (eight ranks share the GPU; the reduce-scatter
+# bench.py's G=8 round (default: c4 strong, n=1024 in total, plus the sharded c5) on a one-GPU box (eight ranks share the GPU; the reduce-scatter
 # runs over gloo on host copies because RCCL refuses duplicate devices).  Full c4 sizes per rank
 # (N = 8192 clients, 4 GiB of rows per rank): checks the G=8 client/slot sharding, the N=8192 seed
 # table and the out == |U| invariant across ranks, not the timing.
