@@ -67,6 +67,42 @@ def test_reconstruction_end_to_end(eng, N, L, n_off, T, committee):
         assert R["D"] > 0
 
 
+def test_reconstruction_first_run_behind_a_long_kernel(eng):
+    """A fresh ServerReconstruction's FIRST run() (its buffers, and the fills of the self-mask
+    signs and the queue counters, made then) with a long kernel already queued on the caller's
+    stream: the CU-partitioned streams wait on the caller's `ready` event, so they must not read
+    a buffer whose fill is still queued behind that kernel."""
+    import torch
+    from flamingo_amd.reconstruct import ServerReconstruction
+    N, L = 256, 20000
+    m = np.frombuffer(b"".join(P.bench_seed("recon1", i) for i in range(N)), np.uint8).reshape(N, 32)
+    nbrs = P.synthetic_neighbors(N, degree=8, seed=5)
+    off = np.arange(3, N, 37)
+    on = np.setdiff1d(np.arange(N), off)
+    R = recovery_round(eng, m, nbrs, on, off, T=5, committee=12, seed=4)
+    dev = torch.device("cuda:0")
+    rows = torch.empty((N, L), dtype=torch.int32, device=dev)
+    eng.client_mask_dev(R["seg"], torch.from_numpy(R["client_seeds"]).to(dev), R["client_signs"], rows, L)
+    r_on = rows[torch.from_numpy(on).to(dev)].contiguous()
+    t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares", "pair_signs")}
+    caller = torch.cuda.Stream()
+    for kw in (dict(ec_cus=24, cu_pick="first", pass1_min_items=4096, pair_queue=True, ec_terms=2),
+               dict(ec_cus=24, cu_pick="first", pass1_min_items=4096)):
+        torch.cuda.synchronize()
+        rec = ServerReconstruction(eng, **kw)
+        out = torch.empty(L, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(caller):
+            big = torch.ones((4096, 4096), device=dev)
+            for _ in range(8):
+                big = big @ big * 1e-4       # a few ms queued ahead of the run on the caller's stream
+            rec.run(r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out,
+                    stream=caller)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy().view(np.uint32)
+        assert np.all(o == len(on)), (kw, np.flatnonzero(o != len(on))[:8])
+        rec.close()
+
+
 @pytest.mark.parametrize("K,L", [(37, 5000), (100, 1 << 16), (1, 1024), (16, 17)])
 @pytest.mark.parametrize("stop", ["never", "at_once"])
 def test_pair_units_queue_vs_oracle(eng, K, L, stop):

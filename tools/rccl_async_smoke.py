@@ -48,6 +48,26 @@ for comm in ("torch", "rccl"):
                 print(f"{comm} rep {rep} round {i + 1}: out==want {e}  partial==want {bool(torch.equal(p_, w))} "
                       f"mismatches {int((o != w).sum())}", flush=True)
                 ok &= e
+# launch() with a stream that is NOT torch's current stream (the kernel, the collective and the
+# buffer reuse must all order against `stream`, not the current one): a long kernel is queued on
+# `stream` first so an unordered collective would read a partial before it is written
+side = torch.cuda.Stream()
+for comm in ("torch", "rccl"):
+    pipe = ShardedRound(eng, L, buffers=2, comm=comm)
+    pipe._async_ok = lambda: True
+    big = torch.randint(0, 100, (4096, 4096), device="cuda", dtype=torch.float32, generator=g)
+    with torch.cuda.stream(side):            # current stream: `side`; the round runs on `stream`
+        for rep in range(2):
+            with torch.cuda.stream(stream):
+                for _ in range(8):
+                    big = big @ big * 1e-4   # ~ms of work ahead of the round on `stream`
+            bufs = [pipe.launch(r, seeds, signs, stream) for r in rows]
+            torch.cuda.synchronize()
+            got = [pipe._outs[b][:L] for b in bufs[-2:]]
+            for i, (o, w) in enumerate(zip(got, want[1:])):
+                e = bool(torch.equal(o, w))
+                print(f"{comm} non-current stream rep {rep} round {i + 1}: out==want {e}", flush=True)
+                ok &= e
 print(f"rccl async pipelined rounds ok={ok}", flush=True)
 dist.destroy_process_group()
 eng.close()
