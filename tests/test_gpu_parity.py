@@ -542,3 +542,27 @@ def test_client_mask_small_vs_oracle(eng, mode):
                 assert np.all(out[:, L:].cpu().numpy() == 0x3C3C3C3C), (case, "wrote past L")
     finally:
         eng.set_tuning("small", 1)
+
+
+def test_seed_table_not_reused_after_another_entry_point(eng):
+    """flm_aggregate_dev unmasks against the table flm_seed_table_dev published; an entry point
+    that rebuilds the device seed table in between (prg expansion, client masking, pair units)
+    invalidates it, so a stale-table aggregate fails loudly instead of using other seeds
+    (ADVICE r1)."""
+    import torch
+    K, L = 12, 4096
+    g = np.random.Generator(np.random.PCG64(21))
+    seeds = torch.from_numpy(g.integers(0, 256, (K, 32), dtype=np.uint8)).cuda()
+    signs = torch.from_numpy(np.where(g.integers(0, 2, K) == 1, 1, -1).astype(np.int8)).cuda()
+    other = torch.from_numpy(g.integers(0, 256, (K, 32), dtype=np.uint8)).cuda()
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.seed_table_dev(seeds, signs)
+    eng.aggregate_dev(None, K, out, L=L)         # the published table: fine
+    torch.cuda.synchronize()
+    want = O.aggregate_unmask(np.zeros((0, 1), np.uint32), seeds.cpu().numpy(), signs.cpu().numpy(), L=L)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    expanded = torch.empty((K, L), dtype=torch.int32, device="cuda")
+    eng.prg_expand_dev(other, expanded, L)       # rebuilds the table with the same K
+    with pytest.raises(RuntimeError, match="seed table"):
+        eng.aggregate_dev(None, K, out, L=L)
+    torch.cuda.synchronize()
