@@ -44,6 +44,7 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 G
 # clock for the c4 and the mask-only launch.
 PROBE_CHACHA_CEILING_GWORDS = 733.0
 CPI_SUMMARY = "profiles/r02_clock_cpi_summary.json"
+CHACHA_MIX_CPI = 8.0 / 3.0       # cycles per VALU instruction of the add/xor/rotate mix at 2/2/4 cycles
 CHACHA_OPS_PER_WORD = 61.5       # VALU instructions per mask word in items_kernel (PMC: 1.031e9 wave-instructions x 64 / 2^30 words, profiles/r02_profile_summary.json)
 
 
@@ -238,6 +239,10 @@ def main():
         "roofline_valu": {"bound": "valu", "mask_words_per_launch": int(words), "ops_per_word": CHACHA_OPS_PER_WORD,
                           "achieved_tops": round(valu_tops, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
                           "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
+                          # the mix's own peak: 4 adds + 4 xors at 2 cycles and 4 rotates at 4 cycles per
+                          # quarter-round step = 2.67 cycles per instruction
+                          "peak_tops_chacha_mix": round(VALU_PEAK_TOPS * 2.0 / CHACHA_MIX_CPI, 1),
+                          "frac_of_chacha_mix_peak": round(valu_tops / (VALU_PEAK_TOPS * 2.0 / CHACHA_MIX_CPI), 4),
                           "mask_gwords_per_s": round(words / (kms * 1e-3) / 1e9, 1),
                           "probe_chacha_ceiling_gwords": PROBE_CHACHA_CEILING_GWORDS,
                           "probe_source": "profiles/r01_issue_probe.log (QR8 lockstep: 3.52 cycles per instruction at "
