@@ -895,6 +895,11 @@ hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, i
     return hipGetLastError();
 }
 
+// cache-policy bits of the production (merged) variant's row loads; overridable for A/B builds
+// (gfx950 buffer cpol: 1 = sc0, 2 = nt, 16 = sc1)
+#ifndef FLM_ROW_AUX
+#define FLM_ROW_AUX 0
+#endif
 template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0, bool SPREAD = false>
 static void launch_items_t(const Item *d_items, int n_items, const uint32_t *d_rows, uint64_t row_pitch,
                            const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out, hipStream_t stream) {
@@ -912,7 +917,7 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
     switch (variant) {                                               \
         case kVarCoalesced: FLM_L(S, false, false, 4); break;        \
         case kVarBlock: FLM_L(S, true, false, 4); break;             \
-        case kVarMerged: FLM_L(S, true, true, 4); break;             \
+        case kVarMerged: FLM_L(S, true, true, 4, 2, FLM_ROW_AUX); break; \
         case kVarMergedW8: FLM_L(S, true, true, 8); break;           \
         case kVarMergedRU4: FLM_L(S, true, true, 4, 4, 0); break;    \
         case kVarMergedNT: FLM_L(S, true, true, 4, 2, 2); break;     \
