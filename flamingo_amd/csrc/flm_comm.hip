@@ -241,6 +241,8 @@ struct flm_group {
         uint32_t *partial = nullptr, *shard = nullptr;
         size_t cap_partial = 0, cap_shard = 0;
         hipEvent_t done = nullptr;
+        hipEvent_t xdone = nullptr;  // loopback: this rank's shard_sum (it reads every rank's partial)
+        bool xpending = false;
     };
     std::vector<Rank> rk;
     std::string err;
@@ -284,6 +286,8 @@ int exchange(flm_group *g, uint64_t S, const std::vector<uint32_t *> &shards) {
                     return gfail(g, FLM_EHIP, "hipStreamWaitEvent");
             hipError_t e = flm::launch_shard_sum(parts.data(), G, (uint64_t)r * S, S, shards[r], s);
             if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("shard_sum: ") + hipGetErrorString(e));
+            if (hipEventRecord(g->rk[r].xdone, s) != hipSuccess) return gfail(g, FLM_EHIP, "hipEventRecord");
+            g->rk[r].xpending = true;
         }
         return 0;
     }
@@ -295,6 +299,17 @@ int exchange(flm_group *g, uint64_t S, const std::vector<uint32_t *> &shards) {
     const ncclResult_t e2 = rc->GroupEnd();
     if (e != ncclSuccess || e2 != ncclSuccess)
         return gfail(g, FLM_EHIP, std::string("ncclReduceScatter: ") + rc->GetErrorString(e != ncclSuccess ? e : e2));
+    return 0;
+}
+
+// Loopback: rank r's next round rewrites its partial, which the other ranks' shard_sum of the
+// previous round read on their own streams; make stream r wait for those reads first.
+int wait_previous_exchange(flm_group *g, int r) {
+    if (!g->loopback) return 0;  // RCCL: the collective is ordered on each rank's own stream
+    hipStream_t s = flm::rt::stream_of(g->ctx[r]);
+    for (int q = 0; q < g->n; ++q)
+        if (q != r && g->rk[q].xpending && hipStreamWaitEvent(s, g->rk[q].xdone, 0) != hipSuccess)
+            return gfail(g, FLM_EHIP, "hipStreamWaitEvent");
     return 0;
 }
 
@@ -330,7 +345,8 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
         }
         g->ctx.push_back(c);
         (void)hipSetDevice(g->dev[r]);
-        if (hipEventCreateWithFlags(&g->rk[r].done, hipEventDisableTiming) != hipSuccess) {
+        if (hipEventCreateWithFlags(&g->rk[r].done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->rk[r].xdone, hipEventDisableTiming) != hipSuccess) {
             flm_group_free(g);
             return gfail(nullptr, FLM_EHIP, "flm_group_init: hipEventCreate");
         }
@@ -367,6 +383,7 @@ void flm_group_free(flm_group *g) {
         if (g->rk[r].partial) (void)hipFree(g->rk[r].partial);
         if (g->rk[r].shard) (void)hipFree(g->rk[r].shard);
         if (g->rk[r].done) (void)hipEventDestroy(g->rk[r].done);
+        if (g->rk[r].xdone) (void)hipEventDestroy(g->rk[r].xdone);
         flm_free(g->ctx[r]);
     }
     delete g;
@@ -408,6 +425,8 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
         if (int rc = grow(g, r, g->rk[r].shard, g->rk[r].cap_shard, S)) return rc;
     }
+    for (int r = 0; r < G; ++r)
+        if (int rc = wait_previous_exchange(g, r)) return rc;
     std::vector<int> rcs(G, 0);
     auto work = [&](int r) {
         int c0, c1;
@@ -456,6 +475,8 @@ int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, 
     const uint64_t Lp = padded_len(L, G), S = Lp / G;
     for (int r = 0; r < G; ++r)
         if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
+    for (int r = 0; r < G; ++r)
+        if (int rc = wait_previous_exchange(g, r)) return rc;
     for (int r = 0; r < G; ++r) {
         size_t lo, hi;
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);

@@ -64,7 +64,8 @@ class ShardedReconstruction:
 
     def _all_gather(self, chunk, gathered, stream):
         if self.world == 1:
-            gathered[: chunk.shape[0]].copy_(chunk)
+            with torch.cuda.stream(stream):             # torch copies run on the CURRENT stream
+                gathered[: chunk.shape[0]].copy_(chunk)
         elif self.comm == "rccl":
             self.eng.all_gather_dev(chunk, gathered, stream=stream)
         else:
@@ -78,7 +79,8 @@ class ShardedReconstruction:
 
     def _reduce_scatter(self, part, out, stream):
         if self.world == 1:
-            out[: self.L].copy_(part[: self.L])
+            with torch.cuda.stream(stream):
+                out[: self.L].copy_(part[: self.L])
         elif self.comm == "rccl":
             self.eng.reduce_scatter_dev(part, out, self.S, stream=stream)
         else:

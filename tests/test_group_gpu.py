@@ -70,6 +70,31 @@ def test_group_device_round_vs_oracle(G):
         assert np.array_equal(got, want)
 
 
+def test_group_device_rounds_back_to_back():
+    """Two loopback device rounds enqueued without a sync between them: round B's kernels rewrite
+    the partials that round A's exchange reads on the other ranks' streams (the group orders them)."""
+    import torch
+    from flamingo_amd import DeviceGroup
+    from flamingo_amd.engine import client_bounds, shard_bounds
+    G, N, K, L = 4, 24, 30, 1 << 18
+    dev = torch.device("cuda", 0)
+    cases = [case(N, K, L, 901), case(N, K, L, 902)]
+    with DeviceGroup([0] * G) as grp:
+        ins, outs = [], []
+        for rows, seeds, signs in cases:
+            d_rows = [torch.from_numpy(rows[slice(*client_bounds(N, G, r))].view(np.int32)).to(dev) for r in range(G)]
+            ins.append((d_rows, [torch.from_numpy(seeds).to(dev)] * G, [torch.from_numpy(signs).to(dev)] * G))
+            outs.append([torch.zeros((shard_bounds(L, G, r)[2],), dtype=torch.int32, device=dev) for r in range(G)])
+        torch.cuda.synchronize()
+        for (d_rows, d_seeds, d_signs), shards in zip(ins, outs):
+            grp.aggregate_unmask_dev(d_rows, d_seeds, d_signs, shards, L)
+        grp.sync()
+        for (rows, seeds, signs), shards in zip(cases, outs):
+            got = np.concatenate([shards[r][: shard_bounds(L, G, r)[1] - shard_bounds(L, G, r)[0]].cpu().numpy()
+                                  for r in range(G)]).view(np.uint32)
+            assert np.array_equal(got, O.aggregate_unmask(rows, seeds, signs, threads=8))
+
+
 def test_group_reproduces_reference_round(ref, refnpz):
     """The reference's own round (tests/golden/make_ref_golden.py) through a 4-rank group."""
     from flamingo_amd import DeviceGroup, MaskEngine
