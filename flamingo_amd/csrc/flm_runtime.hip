@@ -113,7 +113,8 @@ struct flm_ctx {
     int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
-    int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms)
+    int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
+                             // 2 same-tile window items (plan_window_same; 0.228 vs 0.188 ms at G = 8, r02_ab_window_same.log)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
 
@@ -298,6 +299,79 @@ constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this ma
 constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
 constexpr int kWindowItems = 512;         // item target of a windowed (slot-sharded) round: 2 per CU
 
+// A rank of the slot-sharded round as same-tile items (pairing 2).  The shard's 1024-slot tiles
+// carry rows AND seeds, cut into P matching parts (part p of a tile: rows [N p/P, N (p+1)/P) and
+// seeds [K p/P, K (p+1)/P), atomics when P > 1); every other tile is one rows-only item, spread
+// evenly between the heavy items so that row streaming runs beside the ChaCha work from the
+// start.  Every item writes one tile, so the merged single-accumulator kernel runs (63 VGPRs,
+// 8 waves/SIMD) instead of the dual-tile kernel (104 VGPRs, 4 waves/SIMD).  Measured slower than
+// the dual-tile items at G = 2 / 4 / 8 (0.78 / 0.42 / 0.228 ms against 0.69 / 0.36 / 0.188 ms,
+// profiles/r02_ab_window_same.log): a tuning option (flm_set_tuning "pairing" 2), not the default.
+void plan_window_same(uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
+                      uint64_t prg_slot0, uint64_t heavy_target, std::vector<Item> &items, Plan &plan) {
+    const uint64_t W = flm::kWaveSlots;
+    const uint64_t tm = (mask_hi - mask_lo + W - 1) / W;
+    uint64_t P = tm ? (heavy_target + tm - 1) / tm : 1;
+    while (P > 1 && (uint64_t)K < 16 * P) P /= 2;  // >= 16 seeds per part: every wave has work
+    if (P < 1) P = 1;
+    std::vector<Item> heavy, light;
+    for (uint64_t t = mask_lo; t < mask_hi; t += W) {
+        const uint32_t valid = (uint32_t)std::min<uint64_t>(W, mask_hi - t);
+        for (uint64_t p = 0; p < P; ++p) {
+            Item it;
+            std::memset(&it, 0, sizeof it);
+            const uint32_t ra = (uint32_t)((uint64_t)N * p / P), rb = (uint32_t)((uint64_t)N * (p + 1) / P);
+            const uint32_t sa = (uint32_t)((uint64_t)K * p / P), sb = (uint32_t)((uint64_t)K * (p + 1) / P);
+            const uint32_t at = P > 1 ? (flm::kRowAtomic | flm::kMaskAtomic) : 0u;
+            if (rb > ra) {
+                it.flags |= flm::kHasRows | at;
+                it.row_in = (uint64_t)ra * pitch + t;
+                it.nrows = rb - ra;
+                it.row_out = t;
+                it.row_valid = valid;
+            }
+            if (sb > sa) {
+                it.flags |= flm::kHasMask | at | (rb > ra ? flm::kSameTile : 0u);
+                it.k0 = sa;
+                it.nseeds = sb - sa;
+                it.mask_out = t;
+                it.mask_ctr = (prg_slot0 + t) / 16;
+                it.mask_valid = valid;
+                if (p == 0) it.flags |= flm::kMaskBiasNneg;
+            }
+            if (it.flags) heavy.push_back(it);
+        }
+    }
+    auto rows_only = [&](uint64_t a, uint64_t b) {
+        for (uint64_t t = a; t < b; t += W) {
+            Item it;
+            std::memset(&it, 0, sizeof it);
+            it.flags = flm::kHasRows;
+            it.row_in = t;
+            it.nrows = (uint32_t)N;
+            it.row_out = t;
+            it.row_valid = (uint32_t)std::min<uint64_t>(W, b - t);
+            light.push_back(it);
+        }
+    };
+    rows_only(0, mask_lo);
+    rows_only(mask_hi, L);
+    // interleave: light item j goes after heavy item floor((j + 1) * H / (Lt + 1))
+    const size_t H = heavy.size(), Lt = light.size();
+    items.reserve(H + Lt);
+    size_t j = 0;
+    for (size_t h = 0; h < H; ++h) {
+        items.push_back(heavy[h]);
+        while (j < Lt && (j + 1) * H <= (h + 1) * (Lt + 1)) items.push_back(light[j++]);
+    }
+    while (j < Lt) items.push_back(light[j++]);
+    plan.subtiles = 1;
+    plan.seed_light = false;
+    plan.single_tile = true;
+    plan.needs_zero = P > 1;
+    plan.atomics = P > 1 ? 1 : 0;
+}
+
 // Host-only planning of one aggregate round (no device state): fills `items`
 // and the plan's flags.  Shared by aggregate_plan and the flm_plan_aggregate
 // diagnostic entry point.
@@ -313,6 +387,10 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     // strong-scaled c4 round, G = 8: 0.179 -> 0.169 ms; G = 4: 0.364 -> 0.350-0.360 ms; G = 2 the
     // same (profiles/r02_ab_strong_plan.log).
     const bool windowed = N > 0 && K > 0 && (mask_lo > 0 || mask_hi < L);
+    if (pairing == 2 && windowed && !seed_light && tune_subtiles <= 0) {
+        plan_window_same(pitch, N, K, L, mask_lo, mask_hi, prg_slot0, (uint64_t)min_items, items, plan);
+        return;
+    }
     const int subtiles = tune_subtiles > 0 ? tune_subtiles : ((seed_light || windowed) ? 4 : 1);
     const uint64_t W = (uint64_t)flm::kWaveSlots * subtiles;
     Job j;
@@ -344,7 +422,7 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
     }
     plan.subtiles = subtiles;
     plan.seed_light = seed_light;
-    plan_job(j, pitch, subtiles, pr, pm, pairing == 1, items, plan.needs_zero, plan.atomics, plan.single_tile);
+    plan_job(j, pitch, subtiles, pr, pm, pairing != 0, items, plan.needs_zero, plan.atomics, plan.single_tile);
 }
 
 Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
@@ -1084,7 +1162,7 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
         if (value < -1 || value >= flm::kVarCount) return fail(ctx, FLM_EINVAL, "variant %d out of range", value);
         ctx->tune_variant = value;
     } else if (k == "pairing") {
-        if (value != 0 && value != 1) return fail(ctx, FLM_EINVAL, "pairing must be 0 or 1");
+        if (value < 0 || value > 2) return fail(ctx, FLM_EINVAL, "pairing must be 0, 1 or 2");
         ctx->tune_pairing = value;
     } else if (k == "subtiles") {
         if (value != 0 && value != 1 && value != 4 && value != 16)

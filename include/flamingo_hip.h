@@ -145,8 +145,10 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              (2/3 apply only to plans whose items each write one tile)
  *   "subtiles" 0 auto | 1 | 4 | 16 sub-tiles of 1024 slots per workgroup
  *              for aggregate plans.
- *   "pairing"  0 interleaved single-kind items | 1 dual-tile items (default), for
- *              windows where rows and masks cover different tiles.
+ *   "pairing"  0 interleaved single-kind items | 1 dual-tile items (default) |
+ *              2 same-tile window items (the window's tiles carry rows and seeds in
+ *              matching parts, merged kernel), for windows where rows and masks
+ *              cover different tiles.
  *   "min_items" planner target for work items per aggregate launch
  *              (default 1024; more items = finer load balance, more atomics).
  *   "ec_threads" 64 (default) | 128 | 256 lanes per workgroup of the P-256

@@ -44,6 +44,13 @@ def plan(N, K, L, lo=0, hi=None, pitch=None, prg_slot0=0, subtiles=0, pairing=1)
     (5, 0, 1000, 0, None, 1),                   # rows only
     (33, 33, 4100, 1024, 3072, 1),              # window inside
     (7, 3, 70000, 69984, 70000, 1),             # last block only
+    (128, 1024, 1 << 20, 7 << 17, 8 << 17, 2),  # strong-scaled c4, rank 7 of 8, same-tile window items
+    (256, 1024, 1 << 20, 1 << 18, 2 << 18, 2),  # rank 1 of 4
+    (512, 1024, 1 << 20, 0, 1 << 19, 2),        # rank 0 of 2
+    (1024, 8192, 1 << 20, 3 << 17, 4 << 17, 2),
+    (33, 40, 4100, 1024, 3072, 2),              # window inside, ragged
+    (7, 3, 70000, 69984, 70000, 2),             # last block only (one part)
+    (5, 64, 70000, 4096, 69984, 2),             # fewer rows than parts
 ])
 def test_plan_covers_everything_once(N, K, L, lo, hi, pairing):
     hi = L if hi is None else hi
@@ -113,6 +120,13 @@ def test_plan_modes():
     assert f & 8 and (f >> 8) == 4                         # seed-light: 4096-slot tiles
     _, f, _ = plan(1024, 8192, 1 << 20, 0, 1 << 17)
     assert f & 2 and f & 1 and not f & 4                   # shard: dual-tile, atomics
+    items, f, _ = plan(128, 1024, 1 << 20, 7 << 17, 8 << 17, pairing=2)
+    assert f & 4 and f & 2 and f & 1 and (f >> 8) == 1      # shard as same-tile parts: merged kernel
+    heavy = [(int(it["flags"]) & HAS_MASK) != 0 for it in items]
+    assert sum(heavy) == 128 * 8 and len(items) == 128 * 8 + 896
+    assert heavy[0] and heavy.index(False) <= 3              # rows-only items spread between the heavy ones
+    gaps = np.diff(np.flatnonzero(~np.array(heavy)))
+    assert gaps.max() <= 3
 
 
 def test_pick_cus_balances_xcds():
