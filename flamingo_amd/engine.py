@@ -51,6 +51,28 @@ def _signs_array(signs, K: int) -> np.ndarray:
     return s
 
 
+def _need(cond: bool, msg: str):
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _dev_bytes(t, name: str, cols: int, rows: int, dtype_bytes: int = 1):
+    """A contiguous CUDA tensor of >= rows x cols elements of dtype_bytes each (the kernels index it flat)."""
+    _need(t is not None and t.is_cuda and t.is_contiguous() and t.element_size() == dtype_bytes,
+          f"{name} must be a contiguous CUDA tensor of {dtype_bytes}-byte elements")
+    _need(t.numel() >= rows * cols and (cols == 1 or t.shape[-1] == cols),
+          f"{name} must hold >= {rows} x {cols} elements, got {tuple(t.shape)}")
+
+
+def _dev_rows(rows, L: int) -> int:
+    """Row pitch (elements) of an (N, >= L) 32-bit CUDA tensor whose rows may be a strided view."""
+    _need(rows.is_cuda and rows.dim() == 2 and rows.element_size() == 4, "rows must be a 2-D 32-bit CUDA tensor")
+    _need(rows.shape[1] <= 1 or rows.stride(1) == 1, "rows must be contiguous along a row")
+    pitch = rows.stride(0) if rows.shape[0] > 1 else rows.shape[1]
+    _need(rows.shape[1] >= L and pitch >= rows.shape[1], f"rows must be (N, >= {L}), got {tuple(rows.shape)}")
+    return pitch
+
+
 class MaskEngine:
     """One GPU's mask-and-aggregate engine (a flm_ctx)."""
 
@@ -259,15 +281,20 @@ class MaskEngine:
         rows: (N, pitch) int32/uint32 CUDA tensor (pitch % 4 == 0, pitch >= L);
         seeds: (K, 32) uint8 CUDA tensor; signs: (K,) int8 CUDA tensor;
         out: CUDA tensor with >= L int32/uint32 elements."""
+        # lean checks: this call is the whole host cost of a small round (c2), and every torch
+        # attribute read costs ~0.3 us; the other *_dev wrappers check fully (_dev_bytes, _dev_rows)
         N = rows.shape[0] if rows is not None else 0
-        pitch = rows.shape[1] if N else 0
+        width = rows.shape[1] if N else 0
+        pitch = rows.stride(0) if N > 1 else width          # a strided row view keeps its true pitch
         if L is None:
-            L = pitch
+            L = width
         if mask_hi is None:
             mask_hi = L
         K = seeds.shape[0] if seeds is not None else 0
         if K and (seeds.shape[-1] != 32 or signs.shape[0] < K):
             raise RuntimeError(f"seeds must be (K, 32) with >= K signs, got {tuple(seeds.shape)}, {tuple(signs.shape)}")
+        if width < L or out.numel() < L:
+            raise RuntimeError(f"rows must be (N, >= {L}) and out hold >= {L} elements")
         # plain ints for the c_void_p arguments: this call is the whole host cost of a small
         # round (c2: ~6.5 us of GPU time), so no per-call ctypes wrapper objects
         rc = self.lib.flm_aggregate_unmask_dev(
@@ -283,10 +310,14 @@ class MaskEngine:
         """Capture aggregate_unmask_dev's round as a HIP graph (flm_round_graph_create): one
         hipGraphLaunch per replay.  The tensors are kept alive by the returned object."""
         N = rows.shape[0] if rows is not None else 0
-        pitch = rows.shape[1] if N else 0
-        L = pitch if L is None else L
+        L = (rows.shape[1] if N else 0) if L is None else L
+        pitch = _dev_rows(rows, L) if N else 0
         mask_hi = L if mask_hi is None else mask_hi
         K = seeds.shape[0] if seeds is not None else 0
+        if K:
+            _dev_bytes(seeds, "seeds", 32, K)
+            _dev_bytes(signs, "signs", 1, K)
+        _dev_bytes(out, "out", 1, L, 4)
         h = ctypes.c_void_p()
         rc = self.lib.flm_round_graph_create(
             self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N,
@@ -307,11 +338,12 @@ class MaskEngine:
                       prg_slot0: int = 0, stream=None):
         """Row-sum + unmask kernel against the current seed table (second launch)."""
         N = rows.shape[0] if rows is not None else 0
-        pitch = rows.shape[1] if N else 0
         if L is None:
-            L = pitch
+            L = rows.shape[1] if N else 0
+        pitch = _dev_rows(rows, L) if N else 0
         if mask_hi is None:
             mask_hi = L
+        _dev_bytes(out, "out", 1, L, 4)
         rc = self.lib.flm_aggregate_dev(self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N, K, L,
                                         mask_lo, mask_hi, prg_slot0, ctypes.c_void_p(out.data_ptr()),
                                         self._stream_handle(stream))
@@ -442,7 +474,11 @@ class MaskEngine:
 
     def shamir_combine_dev(self, shares, lambdas, seeds_out, stream=None):
         """Device form: shares (T, M, 32), lambdas (T, 32) uint8 CUDA tensors -> seeds_out (M, 32)."""
+        _need(shares.dim() == 3, "shares must be (T, M, 32)")
         T, M = shares.shape[0], shares.shape[1]
+        _dev_bytes(shares, "shares", 32, T * M)
+        _dev_bytes(lambdas, "lambdas", 32, T)
+        _dev_bytes(seeds_out, "seeds_out", 32, M)
         rc = self.lib.flm_shamir_combine_dev(self.ctx, ctypes.c_void_p(shares.data_ptr()),
                                              ctypes.c_void_p(lambdas.data_ptr()), T, M,
                                              ctypes.c_void_p(seeds_out.data_ptr()), self._stream_handle(stream))
@@ -453,7 +489,17 @@ class MaskEngine:
                        stream=None):
         """Device form: c1 (D,64), shares (T,D,64), lambdas (T,32) uint8 CUDA tensors;
         seeds_out (D,32) uint8 and flags (D,) int32 CUDA tensors are written on `stream`."""
+        _need(shares.dim() == 3, "shares must be (T, D, 64)")
         T, D = shares.shape[0], shares.shape[1]
+        _dev_bytes(shares, "shares", 64, T * D)
+        _dev_bytes(lambdas, "lambdas", 32, T)
+        if c1 is not None:
+            _dev_bytes(c1, "c1", 64, D)
+        if seeds_out is not None:
+            _dev_bytes(seeds_out, "seeds_out", 32, D)
+        if points_out is not None:
+            _dev_bytes(points_out, "points_out", 64, D)
+        _dev_bytes(flags, "flags", 1, D, 4)
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
         rc = self.lib.flm_ec_combine_dev(self.ctx, vp(c1), vp(shares), vp(lambdas), T, D, 1 if negate else 0,
                                          vp(points_out), vp(seeds_out), vp(flags), self._stream_handle(stream))
@@ -466,6 +512,14 @@ class MaskEngine:
         dst (>= L) int32, ws (>= 2) int32 CUDA tensors.  final=False adds the units claimed before
         ws[1] is set into dst; final=True writes dst = p0 + p1 plus the units left."""
         K = seeds.shape[0] if seeds is not None else 0
+        if K:
+            _dev_bytes(seeds, "seeds", 32, K)
+            _dev_bytes(signs, "signs", 1, K)
+        _dev_bytes(dst, "dst", 1, L, 4)
+        _dev_bytes(ws, "ws", 1, 2, 4)
+        for name, t in (("p0", p0), ("p1", p1)):
+            if t is not None:
+                _dev_bytes(t, name, 1, L, 4)
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)  # noqa: E731
         rc = self.lib.flm_pair_units_dev(self.ctx, vp(seeds), vp(signs), K, vp(p0), vp(p1), vp(dst), L, vp(ws),
                                          1 if final else 0, int(groups), self._stream_handle(stream))
@@ -641,8 +695,19 @@ class DeviceGroup:
         """rows/seeds/signs/shards: per-rank CUDA tensors on the ranks' devices (rows (N_r, pitch) with one
         common pitch; shards >= S words).  Enqueued on the ranks' streams; call sync() before reading."""
         n = self.n
-        pitch = max((r.shape[1] for r in rows if r is not None and r.shape[0]), default=0)
+        _need(len(rows) == n and len(shards) == n and len(seeds) == n and len(signs) == n,
+              f"rows, seeds, signs and shards need one entry per rank ({n})")
+        pitches = {_dev_rows(r, L) for r in rows if r is not None and r.shape[0]}
+        _need(len(pitches) <= 1, f"every rank's rows need the same pitch, got {sorted(pitches)}")
+        pitch = pitches.pop() if pitches else 0
         K = seeds[0].shape[0] if seeds and seeds[0] is not None else 0
+        S = shard_bounds(L, n, 0)[2]
+        for r in range(n):
+            if K:
+                _dev_bytes(seeds[r], f"seeds[{r}]", 32, K)
+                _need(seeds[r].shape[0] == K, "every rank needs the same K seeds")
+                _dev_bytes(signs[r], f"signs[{r}]", 1, K)
+            _dev_bytes(shards[r], f"shards[{r}]", 1, S, 4)
         vp = ctypes.c_void_p
         d_rows = (vp * n)(*[r.data_ptr() if r is not None and r.shape[0] else 0 for r in rows])
         n_rows = (ctypes.c_int * n)(*[int(r.shape[0]) if r is not None else 0 for r in rows])

@@ -180,6 +180,54 @@ def test_bad_arguments_raise(eng):
             eng.set_tuning("small", 1)
 
 
+def test_device_wrappers_check_shapes(eng):
+    """The *_dev wrappers refuse tensors the kernels would index past (short outputs, ragged pitches)."""
+    import torch
+    from flamingo_amd import DeviceGroup
+    from flamingo_amd.engine import shard_bounds
+    dev = torch.device("cuda", 0)
+    rows, seeds, signs = rand_case(3, 4, 5, 3000)
+    d_rows = torch.from_numpy(rows.view(np.int32)).to(dev)
+    d_seeds, d_signs = torch.from_numpy(seeds).to(dev), torch.from_numpy(signs).to(dev)
+    with pytest.raises(RuntimeError):
+        eng.aggregate_unmask_dev(d_rows, d_seeds, d_signs, torch.empty(2999, dtype=torch.int32, device=dev), L=3000)
+    eng.seed_table_dev(d_seeds, d_signs)
+    with pytest.raises(RuntimeError):
+        eng.aggregate_dev(d_rows, 5, torch.empty(100, dtype=torch.int32, device=dev), L=3000)
+    T, D, M = 3, 4, 6
+    u8 = lambda *s: torch.zeros(s, dtype=torch.uint8, device=dev)  # noqa: E731
+    with pytest.raises(RuntimeError):
+        eng.shamir_combine_dev(u8(T, M, 32), u8(T, 32), u8(M - 1, 32))
+    with pytest.raises(RuntimeError):
+        eng.ec_combine_dev(u8(D, 64), u8(T, D, 64), u8(T, 32), u8(D, 32), torch.zeros(D - 1, dtype=torch.int32,
+                                                                                      device=dev))
+    with pytest.raises(RuntimeError):
+        eng.pair_units_dev(d_seeds, d_signs, torch.zeros(10, dtype=torch.int32, device=dev), 3000,
+                           torch.zeros(4, dtype=torch.int32, device=dev), 8)
+    with DeviceGroup([0, 0]) as grp:
+        wide = torch.zeros((2, 3072), dtype=torch.int32, device=dev)
+        S = shard_bounds(3000, 2, 0)[2]
+        shards = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(2)]
+        with pytest.raises(RuntimeError, match="pitch"):
+            grp.aggregate_unmask_dev([d_rows[:2], wide], [d_seeds] * 2, [d_signs] * 2, shards, 3000)
+        with pytest.raises(RuntimeError):
+            grp.aggregate_unmask_dev([d_rows[:2], d_rows[2:]], [d_seeds] * 2, [d_signs] * 2,
+                                     [shards[0], shards[1][:S - 1]], 3000)
+
+
+def test_device_round_on_strided_rows(eng):
+    """Rows handed over as a column slice of a wider buffer: the wrapper passes the buffer's true pitch."""
+    import torch
+    N, K, L = 9, 7, 5000
+    rows, seeds, signs = rand_case(4, N, K, L)
+    wide = torch.zeros((N, L + 200), dtype=torch.int32, device="cuda")
+    wide[:, :L] = torch.from_numpy(rows.view(np.int32)).cuda()
+    out = torch.empty(L, dtype=torch.int32, device="cuda")
+    eng.aggregate_unmask_dev(wide[:, :L], torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda(), out, L=L)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), O.aggregate_unmask(rows, seeds, signs, L=L, threads=8))
+
+
 # -------------------------------------------------------- device-resident
 def test_device_windows_sum_to_whole(eng):
     """Slot-sharded unmask: per-shard windows reproduce the whole round."""
