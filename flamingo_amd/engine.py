@@ -293,7 +293,7 @@ class MaskEngine:
         K = seeds.shape[0] if seeds is not None else 0
         if K and (seeds.shape[-1] != 32 or signs.shape[0] < K):
             raise RuntimeError(f"seeds must be (K, 32) with >= K signs, got {tuple(seeds.shape)}, {tuple(signs.shape)}")
-        if width < L or out.numel() < L:
+        if (N and width < L) or out.numel() < L:
             raise RuntimeError(f"rows must be (N, >= {L}) and out hold >= {L} elements")
         # plain ints for the c_void_p arguments: this call is the whole host cost of a small
         # round (c2: ~6.5 us of GPU time), so no per-call ctypes wrapper objects
