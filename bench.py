@@ -101,8 +101,20 @@ def main():
     from flamingo_amd.distributed import ShardedRound, client_bounds, init_rccl
 
     eng = MaskEngine(torch.cuda.current_device())
+    comm = "torch"
     if G > 1 and args.dist_backend == "nccl":
-        init_rccl(eng)          # the library's own RCCL communicator: ncclUint32 reduce-scatter on our stream
+        # the library's own RCCL communicator: ncclUint32 reduce-scatter on our stream.  Should it fail
+        # on any rank, every rank falls back to torch.distributed's collectives (RCCL too, int32 sums)
+        err = ""
+        try:
+            init_rccl(eng)
+        except Exception as e:
+            err = f"{type(e).__name__}: {e}"
+        ok_t = torch.tensor([0 if err else 1], device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        comm = "rccl" if int(ok_t.item()) else "torch"
+        if comm == "torch" and err:
+            print(f"warning: library RCCL communicator unavailable ({err}); using torch.distributed", file=sys.stderr)
     L = 1 << args.log2_L
     strong = not args.weak
     N = args.total_clients if strong else args.clients_per_gpu * G
@@ -140,7 +152,7 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     # two partial buffers: round k's reduce-scatter (RCCL, async) runs under round k+1's kernel
-    rnd = ShardedRound(eng, L, buffers=2 if G > 1 else 1)
+    rnd = ShardedRound(eng, L, buffers=2 if G > 1 else 1, comm=comm)
 
     # the rows are built last, right before the warm-up: the host-side preparation above leaves
     # the GPU idle, and MI355X ramps its clock back up over ~30 ms of load
@@ -286,7 +298,7 @@ def main():
                                              coll_dev)
     if G > 1 and not args.profile and not args.no_configs:
         res["other_configs"] = {"c5": measure_c5_sharded(eng, torch, dist, P, G, rank,
-                                                         backend=args.dist_backend)}
+                                                         backend=args.dist_backend, comm=comm)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if G > 1:
@@ -570,7 +582,7 @@ def mask_only_ceiling(eng, torch, d_seeds, d_signs, L, lo, hi, stream, reps=10):
             "kernel_ms": round(ms, 4), "mask_gwords_per_s": round(words / (ms * 1e-3) / 1e9, 1)}
 
 
-def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, steps=5):
+def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, steps=5, comm=None):
     """BASELINE c5 on G GPUs (n=4096, L=2^20, 1 % dropouts, 10 iterations): every rank runs
     flamingo_amd.dist_recon.ShardedReconstruction on its share -- its online clients' rows, all
     m_i (Shamir), its chunk of the dropout pairs (EC combine on a side stream), one all-gather of
@@ -583,7 +595,7 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
     N, L, T = 4096, 1 << 20, 20
     m = np.frombuffer(b"".join(P.bench_seed("c5", i) for i in range(N)), np.uint8).reshape(N, 32)
     stream = torch.cuda.current_stream()
-    rec = ShardedReconstruction(eng, L, comm="rccl" if backend == "nccl" else "torch")
+    rec = ShardedReconstruction(eng, L, comm=comm or ("rccl" if backend == "nccl" else "torch"))
     out = torch.empty(rec.S, dtype=torch.int32, device=dev)
     per_round, oks, Ds = [], True, []
     cache = {}
@@ -634,7 +646,7 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
             "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
                         "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "
                         "shard; reduce-scatter ("
-                        + ("library RCCL communicator, ncclUint32" if backend == "nccl" else f"torch.distributed {backend}")
+                        + ("library RCCL communicator, ncclUint32" if rec.comm == "rccl" else f"torch.distributed {backend}")
                         + ")"}
 
 
