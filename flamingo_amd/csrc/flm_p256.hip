@@ -669,7 +669,8 @@ __global__ __launch_bounds__(kEcThreads) void ec_mul_straus_kernel(const uint8_t
 // multiplications of each point doubling are spread over the waves, exchanging field elements
 // through LDS between three barriers:
 //   L1  w0: delta = Z^2          w1: gamma = Y^2          w2: s = (Y+Z)^2
-//   L2  w0: t = (X-delta)(X+delta)  w1: beta = X gamma   w2: gamma^2, Z3 = s - gamma - delta
+//   L2  w0: t = (X-delta)(X+delta), 3t   w1: beta = X gamma, 4 beta, 8 beta   w2: 8 gamma^2
+//       w3: Z3 = s - gamma - delta
 //   L3  w0: X3 = (3t)^2 - 8 beta, Y3 = 3t (4 beta - X3) - 8 gamma^2
 // so a doubling costs 4 multiplications of latency instead of 8 (dbl-2001-b, a = -3).  Additions
 // (~43 per scalar) run on wave 0 with the table of odd multiples in LDS.  A scalar multiplication is
@@ -696,48 +697,51 @@ __device__ __forceinline__ Fe xget(const uint32_t *slot, int lane) {
     return a;
 }
 
-// acc = 2 acc in every wave (all four waves hold acc; wave-uniform branches on w)
+// acc = 2 acc in every wave (all four waves hold acc; wave-uniform branches on w).  The additions
+// of the formula sit off wave 0's last level: L2 gives w1 the multiples of beta, w2 those of
+// gamma^2 and w3 the new Z, so L3 is alpha^2 and alpha (4 beta - X3) with four subtractions.
+// Slots: L1 writes 0..2 and the result lands in 6..8, so the next operation's first level (slots
+// 0..2) never overwrites what a wave is still reading.
 __device__ __forceinline__ void coop_dbl(Jac &acc, int w, int lane, uint32_t *S) {
-    Fe d, g, sq, t;
+    Fe alpha;
     if (w == 0) {
-        d = fe_sqr(acc.Z);
-        xput(S + 0 * 512, d, lane);
+        xput(S + 0 * 512, fe_sqr(acc.Z), lane);              // delta
     } else if (w == 1) {
-        g = fe_sqr(acc.Y);
-        xput(S + 1 * 512, g, lane);
+        xput(S + 1 * 512, fe_sqr(acc.Y), lane);              // gamma
     } else if (w == 2) {
-        sq = fe_sqr(fe_add(acc.Y, acc.Z));
+        xput(S + 2 * 512, fe_sqr(fe_add(acc.Y, acc.Z)), lane);  // (Y+Z)^2
     }
     __syncthreads();
     if (w == 0) {
-        t = fe_mul(fe_sub(acc.X, d), fe_add(acc.X, d));
+        const Fe d = xget(S + 0 * 512, lane);
+        const Fe t = fe_mul(fe_sub(acc.X, d), fe_add(acc.X, d));
+        alpha = fe_add(fe_add(t, t), t);
     } else if (w == 1) {
-        xput(S + 2 * 512, fe_mul(acc.X, g), lane);  // beta
-    } else if (w == 2) {
-        g = xget(S + 1 * 512, lane);
-        d = xget(S + 0 * 512, lane);
-        xput(S + 3 * 512, fe_sqr(g), lane);                       // gamma^2
-        xput(S + 4 * 512, fe_sub(fe_sub(sq, g), d), lane);        // Z3
-    }
-    __syncthreads();
-    if (w == 0) {
-        const Fe alpha = fe_add(fe_add(t, t), t);
-        const Fe beta = xget(S + 2 * 512, lane);
+        const Fe beta = fe_mul(acc.X, xget(S + 1 * 512, lane));
         const Fe beta2 = fe_add(beta, beta);
         const Fe beta4 = fe_add(beta2, beta2);
-        const Fe beta8 = fe_add(beta4, beta4);
-        const Fe x3 = fe_sub(fe_sqr(alpha), beta8);
-        const Fe g2 = xget(S + 3 * 512, lane);
-        Fe g8 = fe_add(g2, g2);
+        xput(S + 3 * 512, beta4, lane);
+        xput(S + 4 * 512, fe_add(beta4, beta4), lane);       // 8 beta
+    } else if (w == 2) {
+        const Fe g = xget(S + 1 * 512, lane);
+        Fe g8 = fe_sqr(g);
         g8 = fe_add(g8, g8);
         g8 = fe_add(g8, g8);
-        xput(S + 5 * 512, x3, lane);
-        xput(S + 6 * 512, fe_sub(fe_mul(alpha, fe_sub(beta4, x3)), g8), lane);
+        xput(S + 5 * 512, fe_add(g8, g8), lane);             // 8 gamma^2
+    } else {
+        const Fe d = xget(S + 0 * 512, lane), g = xget(S + 1 * 512, lane), sq = xget(S + 2 * 512, lane);
+        xput(S + 6 * 512, fe_sub(fe_sub(sq, g), d), lane);   // Z3
     }
     __syncthreads();
-    acc.X = xget(S + 5 * 512, lane);
-    acc.Y = xget(S + 6 * 512, lane);
-    acc.Z = xget(S + 4 * 512, lane);
+    if (w == 0) {
+        const Fe x3 = fe_sub(fe_sqr(alpha), xget(S + 4 * 512, lane));
+        xput(S + 7 * 512, x3, lane);
+        xput(S + 8 * 512, fe_sub(fe_mul(alpha, fe_sub(xget(S + 3 * 512, lane), x3)), xget(S + 5 * 512, lane)), lane);
+    }
+    __syncthreads();
+    acc.X = xget(S + 7 * 512, lane);
+    acc.Y = xget(S + 8 * 512, lane);
+    acc.Z = xget(S + 6 * 512, lane);
 }
 
 // acc = sel ? acc + Q : acc (add-2007-bl, Q read from the LDS table) with the field
