@@ -746,13 +746,13 @@ __device__ __forceinline__ void coop_dbl(Jac &acc, int w, int lane, uint32_t *S)
 
 // acc = sel ? acc + Q : acc (add-2007-bl, Q read from the LDS table) with the field
 // multiplications spread over the four waves:
-//   L1  w0: z1z1 = Z1^2   w1: z2z2 = Z2^2   w2: zz = (Z1+Z2)^2, s2' = Y2 Z1   w3: s1' = Y1 Z2
-//   L2  w0: u2 = X2 z1z1  w1: u1 = X1 z2z2  w2: Z3' = zz - z1z1 - z2z2, s2 = s2' z1z1   w3: s1 = s1' z2z2
-//   L3  w0: h = u2 - u1, i = (2h)^2          w3: Z3 = Z3' h
-//   L4  w0: j = h i       w1: v = u1 i       w2: r = 2 (s2 - s1), r^2
-//   L5  w0: X3 = r^2 - j - 2v, r (v - X3)    w1: s1 j
+//   L1  w0: z1z1 = Z1^2   w1: z2z2 = Z2^2   w2: zz = (Z1+Z2)^2   w3: s1' = Y1 Z2
+//   L2  w0: u2 = X2 z1z1  w1: u1 = X1 z2z2  w2: Z3' = zz - z1z1 - z2z2, s2' = Y2 Z1   w3: s1 = s1' z2z2
+//   L3  w0: h = u2 - u1, i = (2h)^2          w2: s2 = s2' z1z1          w3: Z3 = Z3' h
+//   L4  w0: j = h i       w1: v = u1 i, 2v   w2: r = 2 (s2 - s1), r^2
+//   L5  w0: X3 = r^2 - j - 2v, r (v - X3)    w1: 2 s1 j
 //   L6  w0: Y3 = r (v - X3) - 2 s1 j, the exceptional cases (acc or Q at infinity, acc == +-Q)
-// 5 multiplications of latency instead of 16.  Slots (512 words each): A0 B1 C2 D3 E4 F5 G6 H7 I8
+// 5 multiplications of latency instead of 16, one per level (s2' waits for L2, where w2 has room).  Slots (512 words each): A0 B1 C2 D3 E4 F5 G6 H7 I8
 // J9 K10; the result goes to D (X), E (Y), F (Z).
 __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool neg, int w, int lane, uint32_t *S,
                                          const uint32_t *tab) {
@@ -774,7 +774,6 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
         xput(B, z2z2, lane);
     } else if (w == 2) {
         zz = fe_sqr(fe_add(acc.Z, Q.Z));
-        s2a = fe_mul(Q.Y, acc.Z);
     } else {
         s1a = fe_mul(acc.Y, Q.Z);
     }
@@ -789,7 +788,7 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
         z1z1 = xget(A, lane);
         z2z2 = xget(B, lane);
         xput(F, fe_sub(fe_sub(zz, z1z1), z2z2), lane);  // Z3'
-        s2 = fe_mul(s2a, z1z1);
+        s2a = fe_mul(Q.Y, acc.Z);
     } else {
         z2z2 = xget(B, lane);
         xput(G, fe_mul(s1a, z2z2), lane);  // s1
@@ -803,6 +802,8 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
         const Fe h2 = fe_add(h, h);
         i = fe_sqr(h2);
         xput(H, i, lane);
+    } else if (w == 2) {
+        s2 = fe_mul(s2a, z1z1);
     } else if (w == 3) {
         u2 = xget(Dd, lane);
         u1 = xget(E, lane);
@@ -815,7 +816,9 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
         xput(J, j, lane);
     } else if (w == 1) {
         i = xget(H, lane);
-        xput(K, fe_mul(u1, i), lane);  // v
+        v = fe_mul(u1, i);
+        xput(K, v, lane);
+        xput(Dd, fe_add(v, v), lane);  // 2v (Dd's u2 was read at L3; R.X lands there at L6)
     } else if (w == 2) {
         s1 = xget(G, lane);
         Fe r = fe_sub(s2, s1);
@@ -830,20 +833,20 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
         v = xget(K, lane);
         r = xget(A, lane);
         const Fe rr = xget(B, lane);
-        x3 = fe_sub(fe_sub(rr, j), fe_add(v, v));
+        x3 = fe_sub(fe_sub(rr, j), xget(Dd, lane));
         y3a = fe_mul(r, fe_sub(v, x3));
     } else if (w == 1) {
         s1 = xget(G, lane);
         j = xget(J, lane);
-        xput(C, fe_mul(s1, j), lane);  // s1 j
+        const Fe s1j = fe_mul(s1, j);
+        xput(C, fe_add(s1j, s1j), lane);  // 2 s1 j
     }
     __syncthreads();
     // L6
     if (w == 0) {
-        const Fe s1j = xget(C, lane);
         Jac R;
         R.X = x3;
-        R.Y = fe_sub(y3a, fe_add(s1j, s1j));
+        R.Y = fe_sub(y3a, xget(C, lane));
         R.Z = xget(I, lane);
         if (fe_is_zero(acc.Z)) {
             R = Q;
