@@ -113,7 +113,7 @@ hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], u
 // P-256 (flm_p256.hip). d_jac holds T*D Jacobian results as SoA planes [T][24][D].
 hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
                          uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves,
-                         int coop = 0, int terms = 1);
+                         int coop = 0, int terms = 1, unsigned lds_pad = 0);
 // Partial sums the combine's ec_mul leaves per element: T, or ceil(T / terms) with Straus lanes.
 int ec_mul_groups(int T, int terms);
 hipError_t launch_shamir_combine(const uint8_t *d_shares, const uint8_t *d_lambdas, int T, int M, uint8_t *d_out,

@@ -1087,9 +1087,9 @@ __global__ __launch_bounds__(kEcThreads) void shamir_combine_kernel(const uint8_
 
 template <int TPB, int WPE>
 static void launch_ec_mul_t(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
-                            uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream) {
+                            uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, unsigned lds_pad) {
     const size_t n = (size_t)T * D;
-    hipLaunchKernelGGL((ec_mul_kernel<TPB, WPE>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, stream,
+    hipLaunchKernelGGL((ec_mul_kernel<TPB, WPE>), dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), lds_pad, stream,
                        d_points, d_scalars, per_element, T, D, d_jac, d_flags);
 }
 
@@ -1099,16 +1099,16 @@ int ec_mul_groups(int T, int terms) { return terms > 1 ? (T + terms - 1) / terms
 
 hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int per_element, int T, int D,
                          uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop,
-                         int terms) {
+                         int terms, unsigned lds_pad) {
     if (T <= 0 || D <= 0) return hipSuccess;
     if (terms > 1 && !per_element) {
         const size_t n = (size_t)ec_mul_groups(T, terms) * D;
         const dim3 grid((unsigned)((n + kEcThreads - 1) / kEcThreads));
         if (terms == 2)
-            hipLaunchKernelGGL(ec_mul_straus_kernel<2>, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, T, D,
+            hipLaunchKernelGGL(ec_mul_straus_kernel<2>, grid, dim3(kEcThreads), lds_pad, stream, d_points, d_scalars, T, D,
                                d_jac, d_flags);
         else if (terms == 4)
-            hipLaunchKernelGGL(ec_mul_straus_kernel<4>, grid, dim3(kEcThreads), 0, stream, d_points, d_scalars, T, D,
+            hipLaunchKernelGGL(ec_mul_straus_kernel<4>, grid, dim3(kEcThreads), lds_pad, stream, d_points, d_scalars, T, D,
                                d_jac, d_flags);
         else
             return hipErrorInvalidValue;
@@ -1122,9 +1122,9 @@ hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int 
     }
 #define FLM_EC(TPB)                                                                                          \
     switch (waves) {                                                                                         \
-        case 4: launch_ec_mul_t<TPB, 4>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
-        case 8: launch_ec_mul_t<TPB, 8>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
-        default: launch_ec_mul_t<TPB, 1>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream); break; \
+        case 4: launch_ec_mul_t<TPB, 4>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream, lds_pad); break; \
+        case 8: launch_ec_mul_t<TPB, 8>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream, lds_pad); break; \
+        default: launch_ec_mul_t<TPB, 1>(d_points, d_scalars, per_element, T, D, d_jac, d_flags, stream, lds_pad); break; \
     }
     switch (threads) {
         case 64: FLM_EC(64) break;

@@ -109,6 +109,8 @@ struct flm_ctx {
     int tune_min_items = 1024;  // planner target for work items per aggregate launch (kDefaultMinItems)
     int tune_ec_threads = 64;   // ec_mul workgroup size (64/128/256; 64 measured best, 3.29 vs 3.43 ms)
     int tune_ec_waves = 1;      // ec_mul register budget as min waves/SIMD (1 = uncapped, 4, 8)
+    int tune_ec_spread = 0;     // KiB of LDS reserved per 64-lane EC workgroup (0 = none): caps EC waves per CU
+                                // so a CU-masked dispatch spreads them one per SIMD instead of packing two
     int tune_ec_terms = 1;      // combine terms per lane (1, 2, 4: Straus, shared doublings)
     int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
@@ -1177,6 +1179,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;
+    } else if (k == "ec_spread") {
+        if (value < 0 || value > 64) return fail(ctx, FLM_EINVAL, "ec_spread must be in [0, 64] KiB");
+        ctx->tune_ec_spread = value;
     } else if (k == "ec_terms") {
         if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_terms must be 1, 2 or 4");
         ctx->tune_ec_terms = value;
@@ -1245,7 +1250,8 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
     const int terms = ec_coop(ctx, (size_t)T * D) ? 1 : ctx->tune_ec_terms;
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
-                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D), terms));
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D), terms,
+                                    1024u * (unsigned)ctx->tune_ec_spread));
     FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), flm::ec_mul_groups(T, terms), D, negate,
                                        d_points_out, d_seeds_out,
                                        d_flags, s));

@@ -52,11 +52,12 @@ import torch
 
 class ServerReconstruction:
     def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride",
-                 pair_split: float = 0.0, pair_queue: bool = False, ec_terms: int = 1):
+                 pair_split: float = 0.0, pair_queue: bool = False, ec_terms: int = 1, ec_spread: int = 0):
         self.eng = engine
         if ec_terms not in (1, 2, 4):
             raise ValueError("ec_terms must be 1, 2 or 4")
         self.ec_terms = int(ec_terms)
+        self.ec_spread = int(ec_spread)   # KiB of LDS per EC workgroup on the confined CUs (flm_set_tuning ec_spread)
         self.pass1_min_items = pass1_min_items
         if not 0.0 <= pair_split < 1.0:
             raise ValueError("pair_split must be in [0, 1)")
@@ -115,12 +116,14 @@ class ServerReconstruction:
         if self.ec_cus > 0:
             self.eng.set_tuning("ec_coop", 0)
             self.eng.set_tuning("ec_terms", self.ec_terms)
+            self.eng.set_tuning("ec_spread", self.ec_spread)
         try:
             self.eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
         finally:
             if self.ec_cus > 0:
                 self.eng.set_tuning("ec_coop", -1)
                 self.eng.set_tuning("ec_terms", 1)
+                self.eng.set_tuning("ec_spread", 0)
 
     def run(self, rows, L: int, lambdas, mi_shares, c1, pair_shares, pair_signs, out, stream=None,
             overlap: bool = True):

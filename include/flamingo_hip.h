@@ -163,6 +163,8 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
  *              (Straus: the terms share one chain of doublings); ignored when the combine
  *              runs cooperatively.
+ *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
+ *              per-lane combine kernels (caps their workgroups per CU).
  *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or

@@ -27,6 +27,7 @@ ap.add_argument("--threads", type=int, default=64)
 ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
 ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
+ap.add_argument("--spread", type=int, default=0, help="flm_set_tuning ec_spread (KiB of LDS per EC workgroup)")
 ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
 a = ap.parse_args()
 
@@ -44,6 +45,7 @@ eng = MaskEngine(0)
 eng.set_tuning("ec_threads", a.threads)
 eng.set_tuning("ec_coop", a.coop)
 eng.set_tuning("ec_terms", a.terms)
+eng.set_tuning("ec_spread", a.spread)
 c1_t = torch.from_numpy(c1).to(dev)
 sh_t = torch.from_numpy(shares).to(dev)
 lam_t = torch.from_numpy(C.scalars_to_wire(lams)).to(dev)

@@ -32,7 +32,7 @@ out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
 rec = ServerReconstruction(eng, pass1_min_items=int(os.environ.get("MIN_ITEMS", "4096")),
                            ec_cus=int(os.environ.get("EC_CUS", "24")), cu_pick="first", pair_queue=True,
-                           ec_terms=int(os.environ.get("EC_TERMS", "2")))
+                           ec_terms=int(os.environ.get("EC_TERMS", "2")), ec_spread=int(os.environ.get("EC_SPREAD", "0")))
 args = (r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out)
 
 # instrument: events recorded on the side / part streams around the pieces of _run_queue
