@@ -78,6 +78,19 @@ def test_ec_combine_matches_oracle(eng):
     assert pts2 == E.combine(None, dec, lam, negate=False)[0]
 
 
+def test_ec_combine_with_lds_spread(eng):
+    """ec_spread reserves LDS per workgroup of the per-lane kernels (fewer workgroups per CU): same result."""
+    c1, dec, lam, hs = _threshold_case(D=70, T=5, committee=9, seed=17, builder=E)
+    want = E.combine(c1, dec, lam)
+    eng.set_tuning("ec_spread", 40)
+    try:
+        assert eng.ec_combine(c1, dec, lam) == want
+    finally:
+        eng.set_tuning("ec_spread", 0)
+    with pytest.raises(RuntimeError):
+        eng.set_tuning("ec_spread", 65)
+
+
 def test_ec_combine_edge_cases(eng):
     # T = 0: the point is c1 itself; a result at infinity hashes 64 zero bytes (EccPoint(0,0))
     c1 = [E.G, E.mul(5)]
