@@ -315,6 +315,9 @@ RECON_QUEUE_MIN_ITEMS = 4096  # its pass 1 plan: 4 same-tile row/seed parts per 
                              # 8.17 ms vs 8.28 at 1024 items (profiles/r02_recon_minitems.log)
 RECON_QUEUE_EC_FRAC = 24 / 256  # EC CUs of the pair-queue schedule, with RECON_QUEUE_EC_TERMS combine terms per lane
 RECON_QUEUE_EC_TERMS = 2        # (Straus): 16 / 24 / 32 CUs -> 9.78 / 8.05 / 8.28 ms; one term per lane on 32 CUs
+RECON_STRIDE_EC_FRAC = 32 / 256  # the same queue schedule with the EC CUs strided over the logical ids: alone, the
+                                 # combine runs 3.84 ms on 24 strided CUs against 5.36 on the first 24
+                                 # (profiles/r02_ec_pick.log); beside the unmask 32 strided CUs measured best
                                 # 8.46 (profiles/r02_straus_recon.log, r02_recon_sweep.log)
 
 
@@ -362,7 +365,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
     per_round, per_round_graph, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], [], True, [], [], [], [], []
-    rec_seq, rec_ovl, rec_cu, rec_q, rec_ok = [], [], [], [], True
+    rec_seq, rec_ovl, rec_cu, rec_q, rec_s, rec_ok = [], [], [], [], [], True
     if recovery:
         from flamingo_amd.reconstruct import ServerReconstruction
         from flamingo_amd.synthetic import recovery_round
@@ -375,6 +378,10 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             max(1, int(round(RECON_QUEUE_EC_FRAC * eng.cu_count())))
         recon_q = ServerReconstruction(eng, dev, pass1_min_items=RECON_QUEUE_MIN_ITEMS, ec_cus=q_cus,
                                        cu_pick="first", pair_queue=True, ec_terms=RECON_QUEUE_EC_TERMS)
+        s_cus = max(1, int(round(RECON_STRIDE_EC_FRAC * eng.cu_count() / 8)) * 8) if eng.cu_count() >= 64 else \
+            max(1, int(round(RECON_STRIDE_EC_FRAC * eng.cu_count())))
+        recon_s = ServerReconstruction(eng, dev, pass1_min_items=RECON_QUEUE_MIN_ITEMS, ec_cus=s_cus,
+                                       cu_pick="stride", pair_queue=True, ec_terms=RECON_QUEUE_EC_TERMS)
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, o, encrypt=eng.chacha20_encrypt)
         n_off = int(round(dropout * N))
@@ -436,7 +443,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             rt = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares",
                                                               "pair_signs")}
             for rc, overlap, acc in ((recon, False, rec_seq), (recon, True, rec_ovl), (recon_cu, True, rec_cu),
-                                     (recon_q, True, rec_q)):
+                                     (recon_q, True, rec_q), (recon_s, True, rec_s)):
                 args = (r_on, L, rt["lambdas"], rt["mi_shares"], rt["c1"], rt["pair_shares"], rt["pair_signs"], out)
                 out.fill_(0)
                 rc.run(*args, stream=stream, overlap=overlap)
@@ -464,14 +471,17 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "overlapped_ms": round(float(np.mean(rec_ovl)), 4),
             "cu_split_ms": round(float(np.mean(rec_cu)), 4),
             "cu_split_queue_ms": round(float(np.mean(rec_q)), 4),
+            "cu_split_queue_strided_ms": round(float(np.mean(rec_s)), 4),
             "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
             "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
                         "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
                         f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS}); "
                         f"cu_split_queue: EC on {recon_q.ec_cus} CUs ({recon_q.ec_terms} combine terms per lane), which then claim pair-mask units from a "
-                        "device work queue until the self-mask pass ends; the last pass takes the rest on all CUs"}
+                        "device work queue until the self-mask pass ends; the last pass takes the rest on all CUs; "
+                        f"cu_split_queue_strided: the same with {recon_s.ec_cus} EC CUs strided over the logical CU ids"}
         recon_cu.close()
         recon_q.close()
+        recon_s.close()
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),

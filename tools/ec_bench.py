@@ -28,6 +28,7 @@ ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
 ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
 ap.add_argument("--spread", type=int, default=0, help="flm_set_tuning ec_spread (KiB of LDS per EC workgroup)")
+ap.add_argument("--pick", default="first", choices=("first", "stride"), help="which CUs --cus selects (pick_cus)")
 ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
 a = ap.parse_args()
 
@@ -54,7 +55,7 @@ pts = torch.empty((a.D, 64), dtype=torch.uint8, device=dev)
 flags = torch.empty(a.D, dtype=torch.int32, device=dev)
 if a.cus:
     from flamingo_amd.reconstruct import pick_cus
-    s = eng.cu_stream(pick_cus(eng.cu_count(), a.cus, "first"))
+    s = eng.cu_stream(pick_cus(eng.cu_count(), a.cus, a.pick))
 else:
     s = torch.cuda.Stream()
 with torch.cuda.stream(s):

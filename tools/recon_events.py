@@ -31,7 +31,7 @@ t = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "
 out = torch.empty(L, dtype=torch.int32, device=dev)
 main = torch.cuda.Stream()
 rec = ServerReconstruction(eng, pass1_min_items=int(os.environ.get("MIN_ITEMS", "4096")),
-                           ec_cus=int(os.environ.get("EC_CUS", "24")), cu_pick="first", pair_queue=True,
+                           ec_cus=int(os.environ.get("EC_CUS", "24")), cu_pick=os.environ.get("EC_PICK", "first"), pair_queue=True,
                            ec_terms=int(os.environ.get("EC_TERMS", "2")), ec_spread=int(os.environ.get("EC_SPREAD", "0")))
 args = (r_on, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out)
 
