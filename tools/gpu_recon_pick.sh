@@ -4,8 +4,8 @@
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 : > gpurun_out/recon_pick.log
-for P in first stride; do
-  for C in 24 32; do
+for P in ${PICKS:-first stride}; do
+  for C in ${CUSET:-24 32}; do
     echo "# pick $P ec_cus $C" >> gpurun_out/recon_pick.log
     EC_PICK=$P EC_CUS=$C timeout -k 10 300 python3 -u tools/recon_events.py 2>/dev/null | grep -v amdgpu >> gpurun_out/recon_pick.log || exit $?
   done
