@@ -238,10 +238,14 @@ class ServerReconstruction:
 
 
 def pick_cus(n: int, k: int, how: str = "stride"):
-    """k of n logical CU ids: evenly strided over the id space, the first k, or "xcd_stride": k/8 per XCD
-    (logical id i sits on XCD i % 8, profiles/r01_cu_map_probe.log) spread over each XCD's CUs."""
+    """k of n logical CU ids: evenly strided over the id space, the first k, "xcd_stride": k/8 per XCD
+    (logical id i sits on XCD i % 8, profiles/r01_cu_map_probe.log) spread over each XCD's CUs, or
+    "xcd": whole XCDs, XCD 0's CUs first."""
     if how == "first":
         return list(range(k))
+    if how == "xcd" and n % 8 == 0 and k <= n:
+        per = n // 8
+        return sorted((i % per) * 8 + i // per for i in range(k))  # whole XCDs: XCD 0's CUs, then XCD 1's, ...
     if how == "xcd_stride" and n % 8 == 0 and k % 8 == 0 and k > 0:
         per, m = n // 8, k // 8
         return sorted(x + 8 * ((j * per) // m) for x in range(8) for j in range(m))

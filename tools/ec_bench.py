@@ -28,7 +28,7 @@ ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
 ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
 ap.add_argument("--spread", type=int, default=0, help="flm_set_tuning ec_spread (KiB of LDS per EC workgroup)")
-ap.add_argument("--pick", default="first", choices=("first", "stride", "xcd_stride"), help="which CUs --cus selects (pick_cus)")
+ap.add_argument("--pick", default="first", choices=("first", "stride", "xcd_stride", "xcd"), help="which CUs --cus selects (pick_cus)")
 ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
 a = ap.parse_args()
 
