@@ -70,17 +70,63 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (c2, c3, c5)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL; the real multi-GPU path) or gloo (test only: ranks sharing one GPU)")
+    ap.add_argument("--no-group", action="store_true", help="skip the single-process device-group leg")
+    ap.add_argument("--group-devices", default="",
+                    help="devices of the device-group leg, e.g. 0,0,0,0 (loopback ranks on one GPU); "
+                         "default every visible GPU")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus: int, env, argv, port: int | None = None):
+    """The command that runs `gpus` ranks of this bench as child processes (torch.distributed.run,
+    one process per GPU, rendezvous on 127.0.0.1), or None when this process is to be the only
+    rank (gpus == 1) or already is one (WORLD_SIZE set by a launcher).  No GPU call happens before
+    this decision: the parent never touches HIP, it only waits for its children."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1, got {gpus}")
+    if gpus == 1 or "WORLD_SIZE" in env:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port or free_port()}",
+            os.path.abspath(__file__), *argv]
+
+
+def world_check(gpus: int, world: int, backend: str, devices: int) -> str:
+    """'' when a run asked for `gpus` ranks may go on with `world`, else why not (the bench then
+    exits non-zero instead of reporting a different n_gpus)."""
+    if gpus != world:
+        return f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+    if backend == "nccl" and world > devices:
+        return f"{world} RCCL ranks need {world} GPUs, {devices} visible (gloo shares one GPU: --dist-backend gloo)"
+    return ""
 
 
 def main():
     args = parse()
+    plan = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if plan is not None:
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("OMP_NUM_THREADS", "1")
+        # rank 0's JSON line reaches stdout straight through the inherited descriptor
+        return subprocess.call(plan, env=env)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    why = world_check(args.gpus, world, args.dist_backend, torch.cuda.device_count())
+    if why:
+        print(f"bench.py: {why}", file=sys.stderr)
+        return 2
     if world > 1:
         dev_id = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev_id)
@@ -90,9 +136,6 @@ def main():
             dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
-    if args.gpus != world and not (world == 1 and args.gpus == 1):
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     G = world
     dev = torch.device("cuda", torch.cuda.current_device())
 
@@ -234,6 +277,11 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u32", "correct": ok,
+        "comm": {"world": G, "backend": args.dist_backend if G > 1 else None,
+                 "collective": (("library RCCL communicator (ncclReduceScatter, ncclUint32)" if rnd.comm == "rccl"
+                                 else f"torch.distributed {args.dist_backend} reduce_scatter_tensor")
+                                if G > 1 else None),
+                 "rccl_comm_ranks": eng.comm_size()[0] if rnd.comm == "rccl" else None},
         "clock_settle": settle,
         "data": "synthetic: valid masked rows y_i = 1 + PRG(m_i) +- PRG(s_ij) made on-GPU from SHA-256 bench "
                 "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
@@ -274,9 +322,18 @@ def main():
     if tr is not None:
         res["roofline"]["traffic"] = tr["bytes"]
         res["roofline"]["traffic_source"] = tr["source"]
+    if not args.profile:
+        pk = practical_peak(eng, torch, rows_on, L, stream)
+        res["roofline"]["practical_peak"] = pk
+        res["roofline"]["frac_of_practical_peak"] = round(ach_gbs / pk["GB/s"], 4)
     if rank == 0 and G == 1 and not args.profile:
         if not args.no_variants:
             res["variants"] = variant_pairs_only(eng, torch, rows_on, m, nbrs, online, L, stream, P)
+            po = res["variants"]["pairs_only"]
+            po["frac_of_practical_peak"] = round(po["GB/s"] / res["roofline"]["practical_peak"]["GB/s"], 4)
+        if not args.no_group:
+            res["group"] = measure_group(torch, P, m, nbrs, online, sseeds, ssigns, L, args.group_devices,
+                                         copy=not args.no_copy)
         if not args.no_configs:
             res["other_configs"] = {
                 "c2": measure_config(eng, torch, P, "c2", N=128, L=16384, o=1, dropout=0.0, check_oracle=True),
@@ -366,6 +423,7 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     out = torch.empty(L, dtype=torch.int32, device=dev)
     per_round, per_round_graph, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], [], True, [], [], [], [], []
     rec_seq, rec_ovl, rec_cu, rec_q, rec_s, rec_ok = [], [], [], [], [], True
+    rep_ms, fp_ovl, fp_q, fp_s = [], [], [], []
     if recovery:
         from flamingo_amd.reconstruct import ServerReconstruction
         from flamingo_amd.synthetic import recovery_round
@@ -455,6 +513,32 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
                 torch.cuda.synchronize()
                 acc.append(q0.elapsed_time(q1) / max(2, steps // 4))
                 rec_ok &= bool(torch.all(out == len(on)).item())
+            # the reference's own split: S = sum of the rows at report time (:346-350), before any
+            # share exists; reconstruction_process then only adds the masks to S (:529-605).  The
+            # latency from the shares to final_sum is the same schedules run over the one row S.
+            S_row = torch.empty((1, L), dtype=torch.int32, device=dev)
+            eng.aggregate_unmask_dev(r_on, None, None, S_row[0], L=L, stream=stream)
+            reps = max(2, steps // 4)
+            q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            q0.record(stream)
+            for _ in range(reps):
+                eng.aggregate_unmask_dev(r_on, None, None, S_row[0], L=L, stream=stream)
+            q1.record(stream)
+            torch.cuda.synchronize()
+            rep_ms.append(q0.elapsed_time(q1) / reps)
+            for rc, acc in ((recon, fp_ovl), (recon_q, fp_q), (recon_s, fp_s)):
+                args = (S_row, L, rt["lambdas"], rt["mi_shares"], rt["c1"], rt["pair_shares"], rt["pair_signs"], out)
+                out.fill_(0)
+                rc.run(*args, stream=stream, overlap=True)
+                q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                q0.record(stream)
+                for _ in range(reps):
+                    rc.run(*args, stream=stream, overlap=True)
+                q1.record(stream)
+                torch.cuda.synchronize()
+                acc.append(q0.elapsed_time(q1) / reps)
+                rec_ok &= bool(torch.all(out == len(on)).item())
+            del S_row
         Ks.append(int(ss.shape[0]))
         Ds.append(int(ss.shape[0] - len(on)))
         oks.append(int(len(on)))
@@ -473,6 +557,15 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
             "cu_split_queue_ms": round(float(np.mean(rec_q)), 4),
             "cu_split_queue_strided_ms": round(float(np.mean(rec_s)), 4),
             "unmask_only_ms": round(ms, 4), "correct": bool(rec_ok),
+            "from_report_partial": {
+                "what": "the reference's split (SA_ServiceAgent.py:346-350 at report, :499-605 at "
+                        "reconstruction): S = sum of the rows computed at report time, before any share "
+                        "exists; the reconstruction schedules then run over the one row S (mask work + "
+                        "EC combine only): the latency from shares-in to final_sum",
+                "report_rows_to_S_ms": round(float(np.mean(rep_ms)), 4),
+                "overlapped_ms": round(float(np.mean(fp_ovl)), 4),
+                "cu_split_queue_ms": round(float(np.mean(fp_q)), 4),
+                "cu_split_queue_strided_ms": round(float(np.mean(fp_s)), 4)},
             "schedule": "overlapped: EC combine on a second stream under the self-mask unmask, pair masks in a "
                         "second pass; cu_split: the same with the two streams CU-partitioned (EC on "
                         f"{recon_cu.ec_cus} CUs, Shamir + self-mask unmask on the rest, min_items {RECON_MIN_ITEMS}); "
@@ -590,6 +683,115 @@ def mask_only_ceiling(eng, torch, d_seeds, d_signs, L, lo, hi, stream, reps=10):
     words = float(K) * (hi - lo)
     return {"what": "mask-only launch of the same K seeds over the same slot window (no rows), same run",
             "kernel_ms": round(ms, 4), "mask_gwords_per_s": round(words / (ms * 1e-3) / 1e9, 1)}
+
+
+def practical_peak(eng, torch, rows, L, stream, reps=10):
+    """The chip's practical HBM read rate measured in the same run: the rows-only launch of the
+    same items_kernel (K = 0: every row summed, no seeds) over the same rows buffer, median of
+    `reps` launches -- the SURVEY 8(d) "read-only stream kernel on the box" denominator."""
+    out = torch.empty(L, dtype=torch.int32, device=rows.device)
+    for _ in range(3):
+        eng.aggregate_unmask_dev(rows, None, None, out, L=L, stream=stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(stream)
+    for i in range(reps):
+        eng.aggregate_unmask_dev(rows, None, None, out, L=L, stream=stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))
+    nbytes = 4.0 * rows.shape[0] * L + 4.0 * L
+    return {"what": "rows-only launch of items_kernel (K = 0) over the same rows, same run, median of "
+                    f"{reps}", "kernel_ms": round(ms, 4), "GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+            "frac_of_spec": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def measure_group(torch, P, m, nbrs, online, sseeds, ssigns, L, spec="", copy=True, steps=20):
+    """The drop-in server's multi-GPU form (Kernel.py:190-271 is ONE process): flm_group over
+    `spec`'s devices (default every visible GPU), the c4 round through
+    flm_group_aggregate_unmask_dev (rows resident on each device: client-sharded rows,
+    slot-sharded masks, one RCCL reduce-scatter over the clique -- no RCCL for one device) and,
+    with copy, flm_group_aggregate_unmask (pinned host rows, one upload thread per device, shards
+    back to the host).  Host-timed per round including the group's launch and sync; checked
+    out == |U| in every slot."""
+    from flamingo_amd import DeviceGroup, PinnedArena, _lib
+    from flamingo_amd.engine import client_bounds, shard_bounds
+    devs = [int(d) for d in spec.split(",")] if spec else list(range(max(1, _lib.load().flm_device_count())))
+    grp = DeviceGroup(devs)
+    G, n_on = grp.n, len(online)
+    try:
+        rows, seeds, signs, shards = [], [], [], []
+        S = shard_bounds(L, G, 0)[2]
+        for r, d in enumerate(devs):
+            dev = torch.device("cuda", d)
+            c0, c1 = client_bounds(n_on, G, r)
+            ids = online[c0:c1]
+            seg_l, cs, cg = [0], [], []
+            for i in ids:
+                cs.append(m[i].tobytes()); cg.append(1)
+                for j in sorted(nbrs[i]):
+                    cs.append(P.synthetic_pair_seed(int(i), j)); cg.append(1 if i < j else -1)
+                seg_l.append(len(cs))
+            rr = torch.empty((len(ids), L), dtype=torch.int32, device=dev)
+            if len(ids):
+                d_cs = torch.from_numpy(np.frombuffer(b"".join(cs), np.uint8).reshape(-1, 32).copy()).to(dev)
+                grp.engines[r].client_mask_dev(np.array(seg_l, np.int64), d_cs, np.array(cg, np.int8), rr, L,
+                                               stream=torch.cuda.current_stream(dev))
+            rows.append(rr)
+            seeds.append(torch.from_numpy(sseeds).to(dev))
+            signs.append(torch.from_numpy(ssigns).to(dev))
+            shards.append(torch.empty(S, dtype=torch.int32, device=dev))
+        for d in set(devs):
+            torch.cuda.synchronize(torch.device("cuda", d))
+
+        def run():
+            grp.aggregate_unmask_dev(rows, seeds, signs, shards, L, after_current=False)
+        t_set = time.perf_counter()
+        n_settle = 0
+        while time.perf_counter() - t_set < 0.2 or n_settle < 3:   # clock settle, then warm-up
+            run()
+            grp.sync()
+            n_settle += 1
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        grp.sync()
+        dt = (time.perf_counter() - t0) / steps
+        ok = True
+        for r in range(G):
+            lo, hi, _ = shard_bounds(L, G, r)
+            ok &= bool(torch.all(shards[r][: hi - lo] == n_on).item())
+        nbytes = 4.0 * n_on * L + 4.0 * L
+        res = {"devices": devs, "ranks": G, "loopback": grp.loopback,
+               "exchange": ("none (one device)" if G == 1 else
+                            "shard_sum kernel (loopback ranks on one GPU)" if grp.loopback else
+                            "ncclReduceScatter over the ncclCommInitAll clique"),
+               "dev": {"what": "flm_group_aggregate_unmask_dev: rows resident, rounds on the ranks' streams, "
+                               "host-timed with flm_group_sync after the last of the rounds",
+                       "ms_per_round": round(dt * 1e3, 4), "GB/s": round(nbytes / dt / 1e9, 1), "correct": ok,
+                       "rounds": steps}}
+        if copy:
+            arena = PinnedArena(int(n_on) * L * 4 + 4096)
+            host = arena.array((n_on, L), np.uint32)
+            o = 0
+            for rr in rows:
+                host.view(np.int32)[o:o + rr.shape[0]] = rr.cpu().numpy()
+                o += rr.shape[0]
+            vecs = [host[i] for i in range(n_on)]
+            best, okc = None, True
+            for _ in range(3):
+                t0 = time.perf_counter()
+                out = grp.aggregate_unmask(vecs, sseeds, ssigns, L=L)
+                t = time.perf_counter() - t0
+                best = t if best is None else min(best, t)
+                okc &= bool(np.all(out == n_on))
+            arena.free()
+            res["host"] = {"what": "flm_group_aggregate_unmask: pinned host rows, each device uploads its "
+                                   "clients over its own link, shards back to host; best of 3",
+                           "ms_per_round": round(best * 1e3, 2), "GB/s": round(nbytes / best / 1e9, 2),
+                           "correct": okc}
+        return res
+    finally:
+        grp.close()
 
 
 def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, steps=5, comm=None):

@@ -28,6 +28,7 @@ SIGNATURES = {
     "flm_free": (None, [_vp]),
     "flm_last_error": (ctypes.c_char_p, [_vp]),
     "flm_version": (ctypes.c_char_p, []),
+    "flm_ctx_stream": (_vp, [_vp]),
     "flm_aggregate_unmask": (_int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),
     "flm_client_mask": (_int, [_vp, _u32p, _int, _i64p, _u8p, _i8p, _sz, _u32p]),
     "flm_prg_expand": (_int, [_vp, _u8p, _int, _sz, _u64, _u32p]),
@@ -59,6 +60,7 @@ SIGNATURES = {
     "flm_stream_destroy": (_int, [_vp, _vp]),
     "flm_shard_bounds": (_int, [_sz, _int, _int, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
     "flm_client_bounds": (_int, [_int, _int, _int, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "flm_rccl_available": (_int, []),
     "flm_comm_unique_id": (_int, [_vp]),
     "flm_comm_init_rank": (_int, [_vp, _int, _int, _vp]),
     "flm_comm_size": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),

@@ -70,21 +70,25 @@ def engine():
 
 def server_devices() -> list:
     """Devices the server's vector steps use: FLM_GROUP_DEVICES ("0,1,2,..."; one id repeated =
-    loopback ranks on one GPU), else FLM_GPUS devices 0..n-1, else every visible GPU."""
+    loopback ranks on one GPU), else FLM_GPUS devices 0..n-1 (FLM_GPUS=all: every visible GPU),
+    else the process's one device (FLM_DEVICE).  A multi-GPU group is opt-in."""
     spec = os.environ.get("FLM_GROUP_DEVICES", "").strip()
     if spec:
         return [int(d) for d in spec.split(",")]
-    n = int(os.environ.get("FLM_GPUS", "0"))
-    if n <= 0:
+    n = os.environ.get("FLM_GPUS", "").strip().lower()
+    if n == "all":
         from ... import _lib
-        n = max(1, int(_lib.load().flm_device_count()))
-    return list(range(n))
+        return list(range(max(1, int(_lib.load().flm_device_count()))))
+    if n and int(n) > 1:
+        return list(range(int(n)))
+    return [int(os.environ.get("FLM_DEVICE", "0"))]
 
 
 def server_engine():
     """The server's partial sum and unmask (SA_ServiceAgent.py:346-350, 529-605) run on every
     device of server_devices(): a DeviceGroup (client-sharded rows, slot-sharded masks, one RCCL
-    reduce-scatter) when that is more than one, else the process MaskEngine."""
+    reduce-scatter) when that is more than one, else the process MaskEngine.  Should the group
+    not come up (RCCL missing, a device refused), the server says so and stays on one GPU."""
     global _group
     devs = server_devices()
     if len(devs) == 1 and devs[0] == int(os.environ.get("FLM_DEVICE", "0")):
@@ -93,7 +97,13 @@ def server_engine():
         from ...engine import DeviceGroup
         if _group is not None:
             _group.close()
-        _group = DeviceGroup(devs)
+            _group = None
+        try:
+            _group = DeviceGroup(devs)
+        except RuntimeError as e:
+            import warnings
+            warnings.warn(f"server device group {devs} unavailable ({e}); using one GPU")
+            return engine()
     return _group
 
 

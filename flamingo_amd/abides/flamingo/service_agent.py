@@ -6,12 +6,14 @@ Four-step round state machine, same as the reference (:123-135):
   2 forward_signatures  forward the committee's signed offline set (DEC)
   3 reconstruction      recover m_i from committee shares; unmask; combine
 
-The hot loops are replaced by calls into the MI355X engine (protocol.server_engine(): every GPU
-of the node through one DeviceGroup, or the one MaskEngine):
-  report_process        S = sum_{i in U} y_i         (:346-350)  -> server_engine().aggregate_unmask(rows, K=0)
+The hot loops are replaced by calls into the MI355X engine (protocol.server_engine(): the one
+MaskEngine, or a DeviceGroup over several GPUs when FLM_GPUS / FLM_GROUP_DEVICES ask for it),
+with the vectors device-resident from arrival to the final sum (flamingo_amd.ingest.VectorStore):
+  receiveMessage VECTOR store y_i on arrival     (:205-210)  -> VectorStore.add (async H2D, pinned ring)
+  report_process        S = sum_{i in U} y_i      (:346-350)  -> VectorStore.partial_sum (S stays on device)
   reconstruction_process
       s_ij for dropout pairs: c1 - sum_j lambda_j (sk_j c0), SHA-256   (:542-585) -> MaskEngine.ec_combine_wire
-      out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> server_engine().aggregate_unmask([S], seeds)
+      out = S - sum PRG(m_i) + sum sigma PRG(s_ij)  (:529-540, :587-605) -> VectorStore.unmask(seeds, signs)
       m_i for online clients: sum_j lambda_j y_{j,i} mod n      (:506-526) -> MaskEngine.shamir_combine
 The vector arithmetic is bit-exact with the reference's numpy uint32 code.
 Message payloads use the reference's JSON formats (wire.py).
@@ -53,7 +55,10 @@ class SA_ServiceAgent(Agent):
         self.users = users
         self.vector_len = param.vector_len
         self.vector_dtype = param.vector_type
-        self.vec_sum_partial = np.zeros(self.vector_len, dtype=self.vector_dtype)
+        self._store = None           # VectorStore: the VECTOR bodies on the GPU(s), from arrival on
+        self._accepting = True       # False between report and the end of reconstruction (:488-497)
+        self._host_partial = np.zeros(self.vector_len, dtype=self.vector_dtype)
+        self.gpu_ms = {}             # iteration -> {"report": ms, "reconstruction": ms} (device time)
         self.final_sum = np.zeros(self.vector_len, dtype=self.vector_dtype)
         self.prime = P256_N
         self.key_length = key_length
@@ -104,6 +109,8 @@ class SA_ServiceAgent(Agent):
                 self.logger.info(f"LATE MSG: VECTOR from iteration {body['iteration']} client {sender}")
                 return
             self.recv_user_vectors[sender] = body["vector"]
+            if self._accepting:
+                self.store().add(sender, body["vector"])        # upload now, overlapping the DES
             self.recv_mi_cipher[sender] = wire.deserialize_tuples_bytes(body["enc_mi_shares"])
             self.recv_pairwise_cipher.update(wire.deserialize_dim1_elgamal(body["enc_pairwise"]))
         elif body["msg"] == "SIGN":
@@ -117,6 +124,22 @@ class SA_ServiceAgent(Agent):
             self.recv_committee_shares_pairwise[sender] = body["shared_result_pairwise"]
             self.recv_committee_shares_mi[sender] = wire.deserialize_dim1_list(body["shared_result_mi"])
             self.recv_recon_index[sender] = body["committee_member_idx"]
+
+    # ------------------------------------------------------- device state
+    def store(self):
+        from ...ingest import VectorStore
+        if self._store is None:
+            self._store = VectorStore(param.server_engine(), self.vector_len, max(1, len(self.users) or
+                                                                                   self.num_clients))
+        return self._store
+
+    @property
+    def vec_sum_partial(self) -> np.ndarray:
+        """S on the host (copied on demand: the round keeps it on the device between report and
+        reconstruction, :346-350 -> :605)."""
+        if self._store is not None and getattr(self._store, "S", None) is not None:
+            return self._store.host_partial()
+        return self._host_partial
 
     # ---------------------------------------------------------------- round
     def initialize(self, currentTime):
@@ -160,12 +183,25 @@ class SA_ServiceAgent(Agent):
         self.client_id_list = list(self.mi_cipher.keys())
         online = set(self.user_vectors.keys())
         offline = set(self.users) - online
-        # partial sum on the GPU (:346-350); the guard mirrors :348-349
-        for cid, v in self.user_vectors.items():
-            if len(v) != self.vector_len:
-                raise RuntimeError("Client sends vector of incorrect length.")
-        self.vec_sum_partial = param.server_engine().aggregate_unmask(list(self.user_vectors.values()), [], [],
-                                                                     L=self.vector_len)
+        # partial sum on the GPU(s) over the rows uploaded at arrival (:346-350); the length guard
+        # of :348-349 raises inside partial_sum.  S stays device-resident until reconstruction.
+        import torch
+        st = self.store()
+        self._accepting = False
+        if st.bad:
+            raise RuntimeError("Client sends vector of incorrect length.")
+        if len(st) != len(self.user_vectors):
+            raise RuntimeError("stored vectors do not match the received ones")
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream(st.devices[0]))
+        t0 = pd.Timestamp("now")
+        done = st.partial_sum()
+        t1 = pd.Timestamp("now")
+        done.synchronize()
+        self.gpu_ms.setdefault(self.current_iteration, {})["report"] = e0.elapsed_time(done)
+        self.agent_print(f"report partial sum: host enqueue {(t1 - t0).total_seconds() * 1e3:.3f} ms, "
+                         f"GPU {e0.elapsed_time(done):.3f} ms ({len(st)} rows on {st.G} device(s), uploaded "
+                         "at arrival)")
         # dropout pairs (online nb, offline id) and their signs (:359-380)
         nbrs = param.neighbors(self.current_iteration, self.num_clients, self.neighborhood_size)
         pairs, signs = P.dropout_pairs(nbrs, online, offline)
@@ -229,6 +265,9 @@ class SA_ServiceAgent(Agent):
         self.user_vectors = {}
         self.committee_shares_pairwise, self.committee_shares_mi, self.recon_index = {}, {}, {}
         self.recv_pairwise_cipher, self.recv_mi_cipher, self.recv_user_vectors = {}, {}, {}
+        if self._store is not None:
+            self._store.reset()
+        self._accepting = True
 
     def reconstruction_process(self):
         self.agent_print("number of collected shares from decryptors:", len(self.committee_shares_mi))
@@ -257,10 +296,13 @@ class SA_ServiceAgent(Agent):
             for s, sg in zip(pair_seeds, self.recon_symbol.values()):
                 seeds.append(bytes(s[: self.key_length]))
                 signs.append(sg)
-        # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU(s): the partial sum is one
-        # more row, and every device regenerates the K masks over its own slot shard only
-        self.final_sum = param.server_engine().aggregate_unmask([self.vec_sum_partial], seeds, signs,
-                                                                L=self.vector_len)
+        # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU(s): every device adds the
+        # K masks over its own slot shard of the device-resident S, then the one copy to the host
+        t0 = pd.Timestamp("now")
+        self.final_sum = self.store().unmask(seeds, signs)
+        ms = (pd.Timestamp("now") - t0).total_seconds() * 1e3
+        self.gpu_ms.setdefault(self.current_iteration, {})["reconstruction_unmask_wall"] = ms
+        self.agent_print(f"reconstruction unmask: {len(seeds)} masks over S on the GPU(s) + D2H, {ms:.3f} ms")
         self.results[self.current_iteration] = self.final_sum
         self.online_counts[self.current_iteration] = len(self.user_vectors)
         self.agent_print("final sum:", self.final_sum)

@@ -55,7 +55,7 @@ struct Rccl {
     const char *(*GetErrorString)(ncclResult_t) = nullptr;
 };
 
-Rccl *rccl() {
+Rccl &rccl_state() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
@@ -88,6 +88,11 @@ Rccl *rccl() {
         FLM_SYM(GetErrorString, "ncclGetErrorString");
 #undef FLM_SYM
     });
+    return r;
+}
+
+Rccl *rccl() {
+    Rccl &r = rccl_state();
     return r.h ? &r : nullptr;
 }
 
@@ -166,6 +171,15 @@ int flm_client_bounds(int N, int n_ranks, int rank, int *c0, int *c1) {
 }
 
 // ======================================================= one process per GPU
+int flm_rccl_available(void) {
+    Rccl *r = rccl();
+    if (!r) {
+        flm::rt::set_error(nullptr, FLM_EHIP, rccl_state().err.c_str());
+        return 0;
+    }
+    return 1;
+}
+
 int flm_comm_unique_id(uint8_t id_out[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
     if (!id_out) return FLM_EINVAL;
@@ -213,7 +227,7 @@ int flm_reduce_scatter_dev(flm_ctx *ctx, const uint32_t *d_send, uint32_t *d_rec
     if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
     if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
     FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : flm::rt::stream_of(ctx);
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as every *_dev call
     FLM_NCCL(ctx, rccl()->ReduceScatter(d_send, d_recv, recv_words, ncclUint32, ncclSum, cs->comm, s));
     return 0;
 }
@@ -224,7 +238,7 @@ int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t se
     if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
     if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
     FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : flm::rt::stream_of(ctx);
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_NCCL(ctx, rccl()->AllGather(d_send, d_recv, send_bytes, ncclUint8, cs->comm, s));
     return 0;
 }
@@ -243,6 +257,7 @@ struct flm_group {
         hipEvent_t done = nullptr;
         hipEvent_t xdone = nullptr;  // loopback: this rank's shard_sum (it reads every rank's partial)
         bool xpending = false;
+        size_t dirty = 0;  // partial words [0, dirty) may hold an earlier round's data
     };
     std::vector<Rank> rk;
     std::string err;
@@ -302,6 +317,21 @@ int exchange(flm_group *g, uint64_t S, const std::vector<uint32_t *> &shards) {
     return 0;
 }
 
+// The reduce-scatter reads partial[r] over all Lp = G*S words; the round writes [0, L).  Words
+// [L, Lp) must be zero: they are at allocation (grow), but an earlier round with a larger L left
+// its sums there, which would reach the last shard's padding.
+int clear_stale_tail(flm_group *g, int r, size_t L) {
+    auto &k = g->rk[r];
+    if (k.dirty > L) {
+        (void)hipSetDevice(g->dev[r]);
+        const size_t hi = std::min(k.dirty, k.cap_partial);
+        hipError_t e = hipMemsetAsync(k.partial + L, 0, (hi - L) * sizeof(uint32_t), flm::rt::stream_of(g->ctx[r]));
+        if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("partial tail: ") + hipGetErrorString(e));
+    }
+    k.dirty = L;
+    return 0;
+}
+
 // Loopback: rank r's next round rewrites its partial, which the other ranks' shard_sum of the
 // previous round read on their own streams; make stream r wait for those reads first.
 int wait_previous_exchange(flm_group *g, int r) {
@@ -351,7 +381,7 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
             return gfail(nullptr, FLM_EHIP, "flm_group_init: hipEventCreate");
         }
     }
-    if (!g->loopback) {
+    if (!g->loopback && n > 1) {  // one device needs no communicator: its shard is the whole vector
         Rccl *r = rccl();
         if (!r) {
             flm_group_free(g);
@@ -419,22 +449,26 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
     if (N < 0 || K < 0) return gfail(g, FLM_EINVAL, "negative N or K");
     if (L == 0) return 0;
     if (!out || (N > 0 && !rows) || (K > 0 && (!seeds || !signs))) return gfail(g, FLM_EINVAL, "NULL argument");
+    int rc_ = 0;
     const int G = g->n;
     const uint64_t Lp = padded_len(L, G), S = Lp / G;
     for (int r = 0; r < G; ++r) {
-        if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
-        if (int rc = grow(g, r, g->rk[r].shard, g->rk[r].cap_shard, S)) return rc;
+        if (G > 1 && (rc_ = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp))) return rc_;
+        if ((rc_ = grow(g, r, g->rk[r].shard, g->rk[r].cap_shard, S))) return rc_;
     }
     for (int r = 0; r < G; ++r)
-        if (int rc = wait_previous_exchange(g, r)) return rc;
+        if ((rc_ = wait_previous_exchange(g, r))) return rc_;
+    for (int r = 0; G > 1 && r < G; ++r)
+        if ((rc_ = clear_stale_tail(g, r, L))) return rc_;
     std::vector<int> rcs(G, 0);
     auto work = [&](int r) {
         int c0, c1;
         size_t lo, hi;
         flm_client_bounds(N, G, r, &c0, &c1);
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
+        // one device: the round writes its shard (the whole vector) directly, no exchange
         rcs[r] = flm::rt::host_round_async(g->ctx[r], rows ? rows + c0 : nullptr, c1 - c0, seeds, signs, K, L, lo, hi,
-                                           g->rk[r].partial);
+                                           G > 1 ? g->rk[r].partial : g->rk[r].shard);
         if (!rcs[r] && hipEventRecord(g->rk[r].done, flm::rt::stream_of(g->ctx[r])) != hipSuccess) rcs[r] = FLM_EHIP;
     };
     if (G == 1) {
@@ -448,7 +482,7 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         if (rcs[r]) return rank_error(g, r, rcs[r]);
     std::vector<uint32_t *> shards(G);
     for (int r = 0; r < G; ++r) shards[r] = g->rk[r].shard;
-    if (int rc = exchange(g, S, shards)) return rc;
+    if (G > 1 && (rc_ = exchange(g, S, shards))) return rc_;
     for (int r = 0; r < G; ++r) {
         size_t lo, hi;
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
@@ -473,20 +507,24 @@ int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, 
     if (L == 0) return 0;
     const int G = g->n;
     const uint64_t Lp = padded_len(L, G), S = Lp / G;
-    for (int r = 0; r < G; ++r)
+    for (int r = 0; G > 1 && r < G; ++r)
         if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
     for (int r = 0; r < G; ++r)
         if (int rc = wait_previous_exchange(g, r)) return rc;
+    for (int r = 0; G > 1 && r < G; ++r)
+        if (int rc = clear_stale_tail(g, r, L)) return rc;
     for (int r = 0; r < G; ++r) {
         size_t lo, hi;
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
         flm_ctx *c = g->ctx[r];
+        // one device: the round writes the caller's shard (the whole vector) directly
         int rc = flm_aggregate_unmask_dev(c, d_rows ? d_rows[r] : nullptr, row_pitch, n_rows[r],
                                           K ? d_seeds[r] : nullptr, K ? d_signs[r] : nullptr, K, L, lo, hi, 0,
-                                          g->rk[r].partial, flm::rt::stream_of(c));
+                                          G > 1 ? g->rk[r].partial : d_shards[r], flm::rt::stream_of(c));
         if (rc) return rank_error(g, r, rc);
         if (hipEventRecord(g->rk[r].done, flm::rt::stream_of(c)) != hipSuccess) return gfail(g, FLM_EHIP, "event");
     }
+    if (G == 1) return 0;
     // the exchange writes the caller's shard buffers directly
     return exchange(g, S, std::vector<uint32_t *>(d_shards, d_shards + G));
 }

@@ -71,6 +71,25 @@ struct Plan {
     int atomics = 0;
     bool single_tile = true;  // every item writes one tile (merged accumulator legal)
     bool seed_light = false;  // mask work small next to row streaming
+    // a cached plan's items are copied in on the stream of its first launch; a launch on
+    // another stream waits for that copy (`ready`) until it is known to have completed
+    hipEvent_t ready = nullptr;
+    hipStream_t up_stream = nullptr;
+    bool ready_known = true;
+};
+
+// Pinned host + device staging for the small per-call tables the *_dev entry points upload
+// (packed seg + signs, signs, work items).  A slot goes back into use only once the launch that
+// read its device copy has completed (its event), so a *_dev call never waits for earlier work:
+// a busy pool grows (up to kStageSlots slots) instead of blocking the host.
+constexpr size_t kStageSlots = 32;
+struct StageSlot {
+    void *host = nullptr;
+    size_t cap = 0;
+    DevBuf dev;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    uint64_t last = 0;
 };
 
 using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>;
@@ -84,12 +103,9 @@ struct flm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    DevBuf rows, out, seeds, signs, segs, recs, meta, bytes_in, bytes_out;
-    // pinned staging for the packed seg + signs of a small client-mask launch; reused once the
-    // copy that read it has completed (event)
-    void *seg_pin = nullptr;
-    size_t seg_pin_cap = 0;
-    hipEvent_t seg_pin_done = nullptr;
+    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out;
+    std::vector<StageSlot *> slots;  // staging pool of the *_dev uploads (StageSlot)
+    uint64_t slot_clock = 0;
     DevBuf ec_in, ec_base, ec_scal, ec_jac, ec_out, ec_dig, ec_flags;  // P-256 batches
     // pinned staging ring for pageable host rows: two buffers, each reused once
     // the DMA that read it has completed (event per buffer)
@@ -101,7 +117,6 @@ struct flm_ctx {
     hipEvent_t copy_done[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t copy_start = nullptr;
     std::map<PlanKey, Plan *> plans;
-    Plan scratch_plan;  // uncached plans (client masking, expansion)
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
     int table_k = -1;  // seeds in the current device seed table
     int tune_variant = -1;   // items_kernel variant, -1 = auto
@@ -142,6 +157,74 @@ int fail(flm_ctx *ctx, int code, const char *fmt, ...) {
     } while (0)
 
 inline uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
+
+// A staging slot of >= `bytes` that no queued work reads any more (StageSlot).  The host
+// waits only when all kStageSlots slots are still queued: then for the oldest.
+StageSlot *stage_acquire(flm_ctx *ctx, size_t bytes, int *rc) {
+    StageSlot *best = nullptr, *free_small = nullptr, *oldest = nullptr;
+    for (StageSlot *s : ctx->slots) {
+        if (s->busy) {
+            const hipError_t q = hipEventQuery(s->done);
+            if (q == hipSuccess) s->busy = false;
+            else if (q != hipErrorNotReady) (void)hipGetLastError();
+        }
+        if (s->busy) {
+            if (!oldest || s->last < oldest->last) oldest = s;
+        } else if (s->cap >= bytes) {
+            if (!best || s->cap < best->cap) best = s;
+        } else if (!free_small) {
+            free_small = s;
+        }
+    }
+    if (!best) {
+        if (ctx->slots.size() < kStageSlots) {
+            best = new StageSlot();
+            if (hipEventCreateWithFlags(&best->done, hipEventDisableTiming) != hipSuccess) {
+                delete best;
+                *rc = fail(ctx, FLM_EHIP, "staging slot: hipEventCreate failed");
+                return nullptr;
+            }
+            ctx->slots.push_back(best);
+        } else if (free_small) {
+            best = free_small;
+        } else {
+            if (hipEventSynchronize(oldest->done) != hipSuccess) {
+                *rc = fail(ctx, FLM_EHIP, "staging slot: hipEventSynchronize failed");
+                return nullptr;
+            }
+            oldest->busy = false;
+            best = oldest;
+        }
+        if (best->cap < bytes) {
+            const size_t want = std::max<size_t>(round_up(bytes, 4096), 4096);
+            if (best->host) (void)hipHostFree(best->host);
+            best->host = nullptr;
+            best->cap = 0;
+            hipError_t e = hipHostMalloc(&best->host, want, hipHostMallocDefault);
+            if (e == hipSuccess) e = best->dev.reserve(want);
+            if (e != hipSuccess) {
+                *rc = fail(ctx, FLM_ENOMEM, "staging slot of %zu bytes: %s", want, hipGetErrorString(e));
+                return nullptr;
+            }
+            best->cap = want;
+        }
+    }
+    best->last = ++ctx->slot_clock;
+    *rc = 0;
+    return best;
+}
+
+// Copy the slot's first `bytes` host bytes to its device buffer on `s`.
+hipError_t stage_upload(StageSlot *slot, size_t bytes, hipStream_t s) {
+    return bytes ? hipMemcpyAsync(slot->dev.p, slot->host, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+}
+
+// The slot is free again once the work enqueued on `s` so far (its readers) has completed.
+hipError_t stage_commit(StageSlot *slot, hipStream_t s) {
+    hipError_t e = hipEventRecord(slot->done, s);
+    if (e == hipSuccess) slot->busy = true;
+    return e;
+}
 
 // ------------------------------------------------------------------ planner
 // Split a job into row units (tiles x row parts) and mask units (tiles x seed
@@ -288,12 +371,35 @@ int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     return v;
 }
 
-int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items) {
+// s == NULL: a synchronous copy (graph capture).  Otherwise the items go through a staging slot
+// on `s` and the plan records `ready` for launches on other streams (run_plan).
+int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items, hipStream_t s = nullptr, bool async = false) {
     plan.n_items = (int)items.size();
     if (items.empty()) return 0;
-    FLM_HIP(ctx, plan.items.reserve(items.size() * sizeof(Item)));
-    FLM_HIP(ctx, hipMemcpy(plan.items.p, items.data(), items.size() * sizeof(Item), hipMemcpyHostToDevice));
+    const size_t bytes = items.size() * sizeof(Item);
+    FLM_HIP(ctx, plan.items.reserve(bytes));
+    if (!async) {
+        FLM_HIP(ctx, hipMemcpy(plan.items.p, items.data(), bytes, hipMemcpyHostToDevice));
+        plan.ready_known = true;
+        return 0;
+    }
+    int rc = 0;
+    StageSlot *slot = stage_acquire(ctx, bytes, &rc);
+    if (!slot) return rc;
+    std::memcpy(slot->host, items.data(), bytes);
+    FLM_HIP(ctx, hipMemcpyAsync(plan.items.p, slot->host, bytes, hipMemcpyHostToDevice, s));
+    FLM_HIP(ctx, stage_commit(slot, s));
+    if (!plan.ready) FLM_HIP(ctx, hipEventCreateWithFlags(&plan.ready, hipEventDisableTiming));
+    FLM_HIP(ctx, hipEventRecord(plan.ready, s));
+    plan.up_stream = s;
+    plan.ready_known = false;
     return 0;
+}
+
+void plan_free(Plan *plan) {
+    plan->items.release();
+    if (plan->ready) (void)hipEventDestroy(plan->ready);
+    delete plan;
 }
 
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
@@ -428,7 +534,7 @@ void build_aggregate_items(int tune_subtiles, int pairing, uint64_t pitch, int N
 }
 
 Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
-                     uint64_t prg_slot0, int *rc) {
+                     uint64_t prg_slot0, hipStream_t s, int *rc) {
     PlanKey key{ctx->tune_subtiles + 100 * ctx->tune_pairing + 1000 * ctx->tune_min_items, pitch, (uint64_t)N,
                 (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
     auto f = ctx->plans.find(key);
@@ -437,10 +543,10 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
     Plan *plan = new Plan();
     build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items,
                           *plan, ctx->tune_min_items);
-    *rc = upload_plan(ctx, *plan, items);
-    if (*rc) { plan->items.release(); delete plan; return nullptr; }
-    if (ctx->plans.size() > 64) {  // bound the cache
-        for (auto &kv : ctx->plans) { kv.second->items.release(); delete kv.second; }
+    *rc = upload_plan(ctx, *plan, items, s, /*async=*/true);
+    if (*rc) { plan_free(plan); return nullptr; }
+    if (ctx->plans.size() > 64) {  // bound the cache (hipFree waits for the launches still reading them)
+        for (auto &kv : ctx->plans) plan_free(kv.second);
         ctx->plans.clear();
     }
     ctx->plans[key] = plan;
@@ -502,8 +608,14 @@ int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sign
 }
 
 // zeroed: the output was already zero-filled on this stream (by the seed-schedule launch)
-int run_plan(flm_ctx *ctx, const Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
+int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
              size_t out_elems, hipStream_t s, bool zeroed = false) {
+    if (!plan.ready_known) {  // the items' copy was enqueued on another stream: order after it
+        const hipError_t q = hipEventQuery(plan.ready);
+        if (q == hipSuccess) plan.ready_known = true;
+        else if (q != hipErrorNotReady) FLM_HIP(ctx, q);
+        else if (s != plan.up_stream) FLM_HIP(ctx, hipStreamWaitEvent(s, plan.ready, 0));
+    }
     if (plan.needs_zero && !zeroed) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
     const int variant_id = pick_variant(ctx, plan);
     FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
@@ -628,8 +740,11 @@ int upload_seeds(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K)
 // Client masking / expansion plan: one job per output row, 16 sub-tiles per
 // workgroup (each wave its own 1024 slots, all of the row's seeds).
 // out[i] = (x[i] or base_bias) + sum of row i's seeds (+1 per negative seed).
+// seg NULL: row i has seed i alone.  signs: K host signs, or NULL for all +1 (expansion).
+// The items and the signs travel in one staging slot (StageSlot): nothing here waits on the host.
 int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, const int64_t *seg, const int8_t *signs,
-                  uint32_t base_bias, size_t L, uint64_t slot0, uint32_t *d_out, hipStream_t s) {
+                  const uint8_t *d_seeds, int K, uint32_t base_bias, size_t L, uint64_t slot0, uint32_t *d_out,
+                  hipStream_t s) {
     const int subtiles = 16;
     std::vector<Item> items;
     bool needs_zero = false, single_tile = true;
@@ -672,16 +787,38 @@ int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, cons
         j.mask_bias = bias;
         plan_job(j, pitch, subtiles, 1, 1, false, items, needs_zero, atomics, single_tile);
     }
-    Plan &plan = ctx->scratch_plan;
+    Plan plan;
     plan.subtiles = subtiles;
     plan.needs_zero = needs_zero;
     plan.atomics = atomics;
     plan.single_tile = single_tile;
-    if (int rc = upload_plan(ctx, plan, items)) return rc;
-    if (needs_zero) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)N * pitch * sizeof(uint32_t), s));
+    plan.n_items = (int)items.size();
+    const size_t item_bytes = items.size() * sizeof(Item);
+    int rc = 0;
+    StageSlot *slot = stage_acquire(ctx, item_bytes + std::max(K, 1), &rc);
+    if (!slot) return rc;
+    uint8_t *h = static_cast<uint8_t *>(slot->host);
+    if (item_bytes) std::memcpy(h, items.data(), item_bytes);
+    if (K > 0) {
+        if (signs) std::memcpy(h + item_bytes, signs, (size_t)K);
+        else std::memset(h + item_bytes, 1, (size_t)K);
+    }
+    FLM_HIP(ctx, stage_upload(slot, item_bytes + (size_t)K, s));
+    const uint8_t *d = slot->dev.as<uint8_t>();
+    rc = run_seed_schedule(ctx, d_seeds, reinterpret_cast<const int8_t *>(d + item_bytes), K, s);
+    if (!rc && needs_zero) {
+        const hipError_t e = hipMemsetAsync(d_out, 0, (size_t)N * pitch * sizeof(uint32_t), s);
+        if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    }
     const int variant_id = pick_variant(ctx, plan);
-    FLM_HIP(ctx, flm::launch_items(subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_x, pitch, ctx->recs.as<SeedRec>(),
-                                   ctx->meta.as<uint32_t>(), d_out, s));
+    if (!rc && plan.n_items) {
+        const hipError_t e = flm::launch_items(subtiles, variant_id, reinterpret_cast<const Item *>(d), plan.n_items,
+                                               d_x, pitch, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s);
+        if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "items launch: %s", hipGetErrorString(e));
+    }
+    // the slot is busy until the work enqueued so far has run, whether or not it all got enqueued
+    FLM_HIP(ctx, stage_commit(slot, s));
+    if (rc) return rc;
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * subtiles;
     ctx->last_atomics = atomics;
@@ -751,18 +888,18 @@ void flm_free(flm_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     flm::comm_release(ctx);
-    for (auto &kv : ctx->plans) {
-        kv.second->items.release();
-        delete kv.second;
-    }
-    ctx->scratch_plan.items.release();
-    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->segs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
+    for (StageSlot *s : ctx->slots) (void)hipEventSynchronize(s->done);  // launches on other streams
+    for (auto &kv : ctx->plans) plan_free(kv.second);
+    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
                       &ctx->bytes_out, &ctx->ec_in, &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out,
                       &ctx->ec_dig, &ctx->ec_flags})
         b->release();
-    if (ctx->seg_pin_done) (void)hipEventSynchronize(ctx->seg_pin_done);
-    if (ctx->seg_pin) (void)hipHostFree(ctx->seg_pin);
-    if (ctx->seg_pin_done) (void)hipEventDestroy(ctx->seg_pin_done);
+    for (StageSlot *s : ctx->slots) {
+        if (s->host) (void)hipHostFree(s->host);
+        s->dev.release();
+        (void)hipEventDestroy(s->done);
+        delete s;
+    }
     for (int i = 0; i < 2; ++i) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
         if (ctx->stage_done[i]) (void)hipEventDestroy(ctx->stage_done[i]);
@@ -776,6 +913,8 @@ void flm_free(flm_ctx *ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
+
+void *flm_ctx_stream(flm_ctx *ctx) { return ctx ? static_cast<void *>(ctx->stream) : nullptr; }
 
 const char *flm_last_error(const flm_ctx *ctx) {
     if (ctx) return ctx->err.c_str();
@@ -838,7 +977,7 @@ int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, in
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
     int rc = 0;
-    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
+    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, s, &rc);
     if (!plan) return rc;
     return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s);
 }
@@ -865,7 +1004,7 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
         ctx->last_variant = kSmallRoundVariant;
         return 0;
     }
-    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, &rc);
+    Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, s, &rc);
     if (!plan) return rc;
     // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
     if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, plan->needs_zero ? d_out : nullptr, L))) return rc;
@@ -1023,34 +1162,25 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     // workgroup per client row.  seg and signs travel in ONE host-to-device copy.
     if (N <= 65535 /* grid.y */ && (ctx->tune_small == 2 || (ctx->tune_small == 1 && (uint64_t)K * L <= (1ull << 26)))) {
         const size_t seg_bytes = (size_t)(N + 1) * sizeof(int64_t), need = seg_bytes + (size_t)K;
-        if (ctx->seg_pin_done) FLM_HIP(ctx, hipEventSynchronize(ctx->seg_pin_done));  // last copy has read it
-        else FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->seg_pin_done, hipEventDisableTiming));
-        if (ctx->seg_pin_cap < need) {
-            if (ctx->seg_pin) FLM_HIP(ctx, hipHostFree(ctx->seg_pin));
-            ctx->seg_pin = nullptr;
-            ctx->seg_pin_cap = 0;
-            FLM_HIP(ctx, hipHostMalloc(&ctx->seg_pin, need, hipHostMallocDefault));
-            ctx->seg_pin_cap = need;
-        }
-        std::memcpy(ctx->seg_pin, seg, seg_bytes);
-        if (K > 0) std::memcpy(static_cast<uint8_t *>(ctx->seg_pin) + seg_bytes, signs, (size_t)K);
-        FLM_HIP(ctx, ctx->segs.reserve(need));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->segs.p, ctx->seg_pin, need, hipMemcpyHostToDevice, s));
-        FLM_HIP(ctx, hipEventRecord(ctx->seg_pin_done, s));
-        FLM_HIP(ctx, flm::launch_small_client_mask(d_x, pitch, N, ctx->segs.as<int64_t>(), d_seeds,
-                                                   reinterpret_cast<const int8_t *>(ctx->segs.as<uint8_t>() + seg_bytes),
-                                                   L, d_x ? 0u : 1u, d_out, s));
+        int rc = 0;
+        StageSlot *slot = stage_acquire(ctx, need, &rc);  // never waits on queued work (StageSlot)
+        if (!slot) return rc;
+        std::memcpy(slot->host, seg, seg_bytes);
+        if (K > 0) std::memcpy(static_cast<uint8_t *>(slot->host) + seg_bytes, signs, (size_t)K);
+        FLM_HIP(ctx, stage_upload(slot, need, s));
+        const hipError_t e = flm::launch_small_client_mask(
+            d_x, pitch, N, slot->dev.as<int64_t>(), d_seeds,
+            reinterpret_cast<const int8_t *>(slot->dev.as<uint8_t>() + seg_bytes), L, d_x ? 0u : 1u, d_out, s);
+        FLM_HIP(ctx, stage_commit(slot, s));
+        FLM_HIP(ctx, e);
         ctx->last_items = (int)(((L + 255) / 256) * (uint64_t)N);
         ctx->last_tile = 256;
         ctx->last_atomics = 0;
         ctx->last_variant = kSmallRoundVariant;
         return 0;
     }
-    // signs go to the device with the seeds (the schedule folds them into xorc)
-    FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
-    if (K > 0) FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, s));
-    if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), (int)K, s)) return rc;
-    return run_rows_jobs(ctx, d_x, pitch, N, seg, signs, 1u, L, 0, d_out, s);
+    // signs go to the device with the work items (the schedule folds them into xorc)
+    return run_rows_jobs(ctx, d_x, pitch, N, seg, signs, d_seeds, (int)K, 1u, L, 0, d_out, s);
 }
 
 int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t slot0, uint32_t *out) {
@@ -1084,13 +1214,8 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     if (int rc = check_range(ctx, slot0 + L)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_HIP(ctx, hipSetDevice(ctx->device));
-    std::vector<int8_t> plus((size_t)K, 1);
-    FLM_HIP(ctx, ctx->signs.reserve((size_t)K));
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, plus.data(), (size_t)K, hipMemcpyHostToDevice, s));
-    if (int rc = run_seed_schedule(ctx, d_seeds, ctx->signs.as<int8_t>(), K, s)) return rc;
-    // the staging vector must outlive the async copy
-    FLM_HIP(ctx, hipStreamSynchronize(s));
-    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, 0u, L, slot0, d_out, s);
+    // +1 signs are written into the staging slot with the work items: no host wait
+    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, d_seeds, K, 0u, L, slot0, d_out, s);
 }
 
 int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *acc, size_t L,

@@ -53,14 +53,44 @@ def client_bounds(N: int, world: int, rank: int):
 def init_rccl(engine, group=None):
     """Attach an RCCL communicator over `group`'s ranks to `engine` (collective).
 
-    Rank 0 makes the unique id (flm_comm_unique_id) and torch.distributed broadcasts it;
-    every rank then joins with flm_comm_init_rank.  Returns (world, rank)."""
-    from .engine import comm_unique_id
+    Every rank makes the same torch.distributed calls in the same order whatever fails, so
+    a failure surfaces as the same RuntimeError on every rank instead of mismatched
+    collectives: (1) all ranks agree that RCCL loads (flm_rccl_available, local);
+    (2) rank 0 makes the unique id and broadcasts (id, error) -- an error on rank 0 reaches
+    everyone; (3) every rank joins with flm_comm_init_rank; (4) all ranks agree it worked.
+    A rank that fails INSIDE ncclCommInitRank leaves the others blocked in RCCL's bootstrap
+    until RCCL's own timeout: that step alone cannot be made recoverable from here.
+    Returns (world, rank)."""
+    from .engine import comm_unique_id, rccl_available
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    box = [comm_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-    engine.comm_init(world, rank, box[0])
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    ok, why = rccl_available()
+    oks = [None] * world
+    dist.all_gather_object(oks, (ok, why), group=group)
+    bad = [f"rank {r}: {w}" for r, (o, w) in enumerate(oks) if not o]
+    if bad:
+        raise RuntimeError("RCCL unavailable on " + "; ".join(bad))
+    box = [None]
+    if rank == 0:
+        try:
+            box = [(comm_unique_id(), "")]
+        except Exception as e:                       # still broadcast: the others are waiting for it
+            box = [(None, f"{type(e).__name__}: {e}")]
+    dist.broadcast_object_list(box, src=src, group=group)
+    uid, err = box[0]
+    if uid is None:
+        raise RuntimeError(f"RCCL unique id on rank 0 failed: {err}")
+    err = ""
+    try:
+        engine.comm_init(world, rank, uid)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err, group=group)
+    bad = [f"rank {r}: {e}" for r, e in enumerate(errs) if e]
+    if bad:
+        raise RuntimeError("flm_comm_init_rank failed on " + "; ".join(bad))
     return world, rank
 
 

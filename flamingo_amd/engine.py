@@ -591,6 +591,14 @@ class PinnedArena:
 
 
 # ------------------------------------------------------------------ multi-GPU
+def rccl_available():
+    """(True, "") when RCCL loads and resolves (flm_rccl_available; local, no GPU work), else (False, why)."""
+    lib = _lib.load()
+    if lib.flm_rccl_available():
+        return True, ""
+    return False, lib.flm_last_error(None).decode()
+
+
 def comm_unique_id() -> bytes:
     """A fresh 128-byte RCCL unique id (flm_comm_unique_id), for rank 0 to broadcast."""
     lib = _lib.load()
@@ -691,9 +699,28 @@ class DeviceGroup:
                     "flm_group_aggregate_unmask")
         return out
 
-    def aggregate_unmask_dev(self, rows, seeds, signs, shards, L: int):
+    def rank_stream(self, r: int):
+        """Rank r's context stream (flm_ctx_stream) as a torch ExternalStream: the group's rounds run there."""
+        import torch
+        cache = self.__dict__.setdefault("_rank_streams", {})
+        if r not in cache:
+            h = self.lib.flm_ctx_stream(self.lib.flm_group_ctx(self.g, r))
+            cache[r] = torch.cuda.ExternalStream(h, device=torch.device("cuda", self.devices[r]))
+        return cache[r]
+
+    def wait(self):
+        """Make torch's current stream on every rank's device wait for that rank's round
+        (no host synchronisation): the shards can then be read in stream order."""
+        import torch
+        for r, d in enumerate(self.devices):
+            torch.cuda.current_stream(torch.device("cuda", d)).wait_stream(self.rank_stream(r))
+
+    def aggregate_unmask_dev(self, rows, seeds, signs, shards, L: int, after_current: bool = True):
         """rows/seeds/signs/shards: per-rank CUDA tensors on the ranks' devices (rows (N_r, pitch) with one
-        common pitch; shards >= S words).  Enqueued on the ranks' streams; call sync() before reading."""
+        common pitch; shards >= S words).  Enqueued on the ranks' context streams and returns.
+        after_current: each rank's stream first waits for torch's current stream on its device, where
+        the inputs were produced (False: the caller has ordered them itself).  Read the shards after
+        sync() (host) or wait() (torch's current streams)."""
         n = self.n
         _need(len(rows) == n and len(shards) == n and len(seeds) == n and len(signs) == n,
               f"rows, seeds, signs and shards need one entry per rank ({n})")
@@ -714,6 +741,10 @@ class DeviceGroup:
         d_seeds = (vp * n)(*[s.data_ptr() if K else 0 for s in seeds])
         d_signs = (vp * n)(*[s.data_ptr() if K else 0 for s in signs])
         d_shards = (vp * n)(*[s.data_ptr() for s in shards])
+        if after_current:
+            import torch
+            for r, d in enumerate(self.devices):
+                self.rank_stream(r).wait_stream(torch.cuda.current_stream(torch.device("cuda", d)))
         self._check(self.lib.flm_group_aggregate_unmask_dev(self.g, d_rows, pitch, n_rows, d_seeds, d_signs, K, L,
                                                             d_shards), "flm_group_aggregate_unmask_dev")
         return shards

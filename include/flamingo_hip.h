@@ -23,7 +23,12 @@
  *  - Host-pointer functions are synchronous: they copy in, compute on the
  *    GPU and copy out; no host pointer is retained after return.
  *  - *_dev functions take device pointers and enqueue work on `stream`
- *    (a hipStream_t; NULL = the HIP null stream) without synchronising.
+ *    (a hipStream_t; NULL = the HIP null stream) and return without waiting
+ *    for earlier work: the small tables they upload (seg/signs, work items)
+ *    go through a pool of pinned staging slots, each reused only after the
+ *    launch that read it has completed.  A context's device seed table is
+ *    shared by its calls: calls of one context on different streams either
+ *    use the same seeds or are ordered by the caller (or use a context each).
  *  - One context per host thread; a context binds one GPU (one process per
  *    GPU).  Create it lazily, after any fork (SA_ServiceAgent.py:562 forks a
  *    multiprocessing.Pool).
@@ -52,6 +57,9 @@ int flm_device_count(void);
 int flm_init(flm_ctx **out, int device);
 void flm_free(flm_ctx *ctx);
 const char *flm_last_error(const flm_ctx *ctx);
+/* The context's own non-blocking stream (a hipStream_t): the host-pointer calls and
+ * the flm_group rounds run on it, so a caller can order its own streams against them. */
+void *flm_ctx_stream(flm_ctx *ctx);
 /* Library / kernel build identification string (static storage). */
 const char *flm_version(void);
 
@@ -284,8 +292,12 @@ int flm_client_bounds(int N, int n_ranks, int rank, int *c0, int *c1);
  * flm_reduce_scatter_dev: d_recv[0..recv_words) = rank's slice of the elementwise
  * uint32 sum over ranks of d_send[0..recv_words*n_ranks).  flm_all_gather_dev:
  * byte all-gather (d_recv = n_ranks * send_bytes), e.g. recovered pair seeds.
- * stream NULL = the context's stream.  flm_comm_size returns 1 when no
- * communicator is attached (then *n_ranks = 1, *rank = 0). */
+ * stream NULL = the HIP null stream, as for every *_dev call.  flm_comm_size
+ * returns 1 when no communicator is attached (then *n_ranks = 1, *rank = 0).
+ * flm_rccl_available: 1 when RCCL could be loaded (dlopen) and every symbol
+ * resolved, else 0 (reason in flm_last_error(NULL)); local, not collective, so
+ * every rank can agree on it before any rank enters flm_comm_init_rank. */
+int flm_rccl_available(void);
 int flm_comm_unique_id(uint8_t id_out[128]);
 int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128]);
 int flm_comm_size(flm_ctx *ctx, int *n_ranks, int *rank);
@@ -305,6 +317,9 @@ int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t se
  * rows at row_pitch on device r; d_seeds[r]/d_signs[r] on device r); enqueues
  * every rank's round and the exchange on the ranks' context streams and
  * returns; d_shards[r] (>= S words on device r) receives slots [lo_r, hi_r).
+ * The rounds run on the ranks' context streams (flm_ctx_stream(flm_group_ctx(g, r))):
+ * the caller orders them after the work that produced the inputs.  A group of
+ * one device needs no RCCL: its round writes the shard (the whole vector) directly.
  * flm_group_sync waits for every rank's stream. */
 typedef struct flm_group flm_group;
 int flm_group_init(flm_group **out, int n, const int *devices);

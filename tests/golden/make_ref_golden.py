@@ -341,7 +341,10 @@ def main():
     for args in (dict(name="A", N=128, L=16384, o=1, offline_per_it=[[3, 77, 100], [13]], parallel_mode=1,
                       keep_recovery=True),
                  dict(name="B", N=128, L=16000, o=1, offline_per_it=[[10, 90]], parallel_mode=0, x_seed=20231015),
-                 dict(name="C", N=128, L=16384, o=1, offline_per_it=[[]], parallel_mode=1)):
+                 dict(name="C", N=128, L=16384, o=1, offline_per_it=[[]], parallel_mode=1),
+                 # BASELINE c3's shape of graph: N = 1024 clients, neighbourhood -o 2 (config/flamingo.py:37-38),
+                 # a few offline clients, so c3's pair ordering and recon_symbol are pinned directly
+                 dict(name="D", N=1024, L=4096, o=2, offline_per_it=[[5, 300, 777, 1000]], parallel_mode=1)):
         rec, arr = run_protocol(**args)
         runs.append(rec)
         arrays.update(arr)

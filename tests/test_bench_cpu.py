@@ -1,0 +1,64 @@
+"""bench.py's launch decision (no GPU): `python bench.py --gpus G` starts G ranks itself, as
+child processes of torch.distributed.run, before any GPU call; a rank started by a launcher
+checks that the world it got is the one asked for, and fails otherwise."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_one_gpu_runs_in_process():
+    assert bench.launch_plan(1, {}, ["--gpus", "1"]) is None
+
+
+def test_ranks_already_launched_run_in_process():
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}, ["--gpus", "8"]) is None
+
+
+def test_multi_gpu_spawns_torchrun_children():
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "2"]
+    cmd = bench.launch_plan(8, {}, argv, port=29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-len(argv) - 1] == os.path.abspath(os.path.join(ROOT, "bench.py"))
+    assert cmd[-len(argv):] == argv            # the children see the same arguments
+
+
+def test_bad_gpu_count_is_refused():
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {}, [])
+
+
+def test_free_port_is_bindable():
+    import socket
+    p = bench.free_port()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", p))
+
+
+@pytest.mark.parametrize("gpus,world,backend,devices,ok", [
+    (1, 1, "nccl", 1, True),
+    (8, 8, "nccl", 8, True),
+    (8, 1, "nccl", 8, False),     # asked for 8, got one rank: must not report n_gpus 1
+    (2, 4, "nccl", 8, False),
+    (4, 4, "nccl", 1, False),     # RCCL ranks need distinct GPUs
+    (4, 4, "gloo", 1, True),      # gloo rehearsal: ranks share one GPU
+])
+def test_world_check(gpus, world, backend, devices, ok):
+    assert (bench.world_check(gpus, world, backend, devices) == "") == ok
+
+
+def test_world_mismatch_exits_nonzero_before_gpu():
+    """A rank told --gpus 4 inside a 2-rank world refuses to run (exit 2, no JSON line)."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "WORLD_SIZE=2" in r.stderr
+    assert r.stdout.strip() == ""

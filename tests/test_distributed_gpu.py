@@ -37,3 +37,19 @@ def test_sharded_reconstruction(nproc, backend):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=dict(os.environ, OMP_NUM_THREADS="4"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "sharded reconstruction ok=True" in r.stdout
+
+
+def test_bench_spawns_its_own_ranks():
+    """`python bench.py --gpus 2` (no torchrun around it) starts two ranks itself and reports
+    n_gpus 2 from a correct round; gloo lets both ranks share the box's one GPU."""
+    import json
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "3", "--warmup", "1", "--log2-L", "16", "--total-clients", "64", "--settle-ms", "0",
+           "--no-cpu", "--no-copy", "--no-variants", "--no-configs", "--no-group"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=dict(os.environ, OMP_NUM_THREADS="4"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["correct"] is True
+    assert res["comm"]["world"] == 2 and res["comm"]["backend"] == "gloo"

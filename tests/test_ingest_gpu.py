@@ -1,0 +1,72 @@
+"""Device-resident VECTOR ingestion (flamingo_amd.ingest.VectorStore) against the oracle.
+
+The store is the drop-in server's path from arrival (SA_ServiceAgent.py:205-210) through the
+partial sum (:346-350) to the final sum (:529-605): rows uploaded at arrival, S kept on the
+device(s), masks added over each device's slot shard.  Checked bit-exactly on one engine and on
+loopback groups (ranks sharing the one GPU), with a duplicate sender, an odd L, growth past the
+initial capacity and a second iteration reusing the rows."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(N, K, L, seed):
+    g = np.random.Generator(np.random.PCG64(seed))
+    rows = g.integers(0, 2**32, (N, L), dtype=np.uint32)
+    seeds = g.integers(0, 256, (K, 32), dtype=np.uint8)
+    signs = np.where(g.random(K) < 0.5, 1, -1).astype(np.int8)
+    return rows, seeds, signs
+
+
+@pytest.mark.parametrize("G", [1, 3])
+@pytest.mark.parametrize("N,K,L", [(20, 9, 16000), (7, 0, 4099), (33, 40, 1 << 17)])
+def test_store_round_vs_oracle(G, N, K, L):
+    from flamingo_amd import DeviceGroup, MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    eng = MaskEngine(0) if G == 1 else DeviceGroup([0] * G)
+    try:
+        st = VectorStore(eng, L, capacity=max(1, N // 2))      # grows past its first capacity
+        for it in range(2):                                      # second iteration reuses the rows
+            rows, seeds, signs = _case(N, K, L, 100 * G + N + it)
+            order = np.random.Generator(np.random.PCG64(it)).permutation(N)
+            junk = np.full(L, 12345, np.uint32)
+            st.add(int(order[0]), junk)                          # overwritten by the same sender below
+            for i in order:
+                st.add(int(i), rows[i])
+            assert len(st) == N
+            st.partial_sum().synchronize()
+            S = rows.sum(axis=0, dtype=np.uint64).astype(np.uint32)
+            assert np.array_equal(st.host_partial(), S)
+            got = st.unmask(seeds, signs)
+            want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+            assert np.array_equal(got, want), (G, N, K, L, it)
+            st.reset()
+    finally:
+        eng.close()
+
+
+def test_store_rejects_a_wrong_length():
+    from flamingo_amd import MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    with MaskEngine(0) as eng:
+        st = VectorStore(eng, 1000, 4)
+        st.add(1, np.zeros(1000, np.uint32))
+        st.add(2, np.zeros(999, np.uint32))
+        with pytest.raises(RuntimeError, match="incorrect length"):
+            st.partial_sum()
+
+
+def test_store_empty_round():
+    from flamingo_amd import MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    with MaskEngine(0) as eng:
+        st = VectorStore(eng, 2048, 4)
+        st.partial_sum().synchronize()
+        assert not st.host_partial().any()
+        s = np.arange(32, dtype=np.uint8).reshape(1, 32)
+        assert np.array_equal(st.unmask(s, [1]), O.prg(s.tobytes(), 2048))

@@ -109,3 +109,55 @@ def test_reconstruction_from_reference_shares(eng, ref, refnpz):
         torch.cuda.synchronize()
         rec.close()
         assert digest(out[:L].cpu().numpy().view(np.uint32)) == it["final_sha256"], kw
+
+
+@pytest.mark.parametrize("run_idx,n_s", [(0, None), (3, 600)])
+def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
+    """The GPU leg of the pair-seed pipeline (SA_ClientAgent.py:256-292), every pair of every
+    client in every iteration of run 0: public keys b_j G and the ECDH points a_i (b_j G) by the
+    batched flm_ec_mul the protocol uses (protocol._ecdh_batch), r_ij = SHA-256 of the point on
+    the GPU (flm_ec_combine with no shares: point = c1, seed = SHA-256(c1)), h_ijt from
+    ChaCha20 on the GPU, hash-to-curve on the host, s_ij = SHA-256 on the GPU -- against the
+    r_ij and s_ij the reference's clients derived from refshim's deterministic pki keys.
+    Run D (N = 1024, -o 2: 40k pairs) checks every r_ij and h_ijt, and s_ij on its first n_s
+    pairs (hash-to-curve is host Python)."""
+    from flamingo_amd import crypto as C
+    from refgold import key_scalar
+    run = ref["runs"][run_idx]
+    N = run["N"]
+    keys = [key_scalar(f"pki_files/client{i}.pem") for i in range(N)]
+    g = np.tile(np.frombuffer(C.point_bytes(C.G), np.uint8), (N, 1))
+    pub, fl = eng.ec_mul_wire(g, C.scalars_to_wire(keys))               # A_j = b_j G, on the GPU
+    assert not fl.any()
+    none_sh, none_l = np.zeros((0, 1, 64), np.uint8), np.zeros((0, 32), np.uint8)
+    for it in run["iterations"]:
+        pre = f"{run['name']}_it{it['iteration']}_"
+        pairs = [(c["id"], j) for c in it["clients"] for j in c["neighbors"]]
+        pts, fl = eng.ec_mul_wire(pub[[j for _, j in pairs]], C.scalars_to_wire([keys[i] for i, _ in pairs]))
+        assert not fl.any()
+        _, r, _ = eng.ec_combine_wire(pts, none_sh.reshape(0, len(pairs), 64), none_l, negate=False)
+        assert np.array_equal(r, refnpz[pre + "r"]), it["iteration"]
+        hs = [str(int.from_bytes(eng.chacha20_encrypt(bytes(x), it["iteration"].to_bytes(16, "big"))[:4], "big")
+                  & 0xFFFF) for x in r]
+        assert hs == [h for c in it["clients"] for h in c["h"]]
+        n = len(hs) if n_s is None else min(n_s, len(hs))
+        H = np.stack([np.frombuffer(C.point_bytes(C.hash_str_to_curve(h)), np.uint8) for h in hs[:n]])
+        _, s, _ = eng.ec_combine_wire(H, none_sh.reshape(0, n, 64), none_l, negate=False)
+        assert np.array_equal(s, refnpz[pre + "s"][:n]), it["iteration"]
+
+
+def test_device_resident_server_matches_reference(eng, ref, refnpz):
+    """The drop-in server's device path (flamingo_amd.ingest.VectorStore: rows stored at arrival,
+    S kept on the GPU, masks added over it) reproduces the reference's S and final_sum."""
+    from flamingo_amd.ingest import VectorStore
+    for run, it in iterations(ref):
+        L = run["L"]
+        seg, seeds, signs = client_table(run, it, refnpz)
+        rows = eng.client_mask(seg, seeds, signs, L, x=client_inputs(run, it))
+        st = VectorStore(eng, L, len(it["arrival"]))
+        for i in it["arrival"]:
+            st.add(i, rows[i])
+        st.partial_sum().synchronize()
+        assert digest(st.host_partial()) == it["S_sha256"]
+        _, _, sseeds, ssigns = server_table(it, refnpz, run)
+        assert digest(st.unmask(sseeds, ssigns)) == it["final_sha256"], (run["name"], it["iteration"])

@@ -1,0 +1,57 @@
+#!/bin/bash
+# The one launcher for GPU sessions (replaces round 1-2's per-session gpu_*.sh scripts).
+#   usage: tools/gpu.sh TAG STEP [STEP ...]      (run through gpurun from the repo root)
+# Steps, each under its own time limit, chained so the first failure ends the session:
+#   tests        pytest -m gpu (whole GPU suite)          -> gpurun_out/TAG_pytest_gpu.log
+#   tests:EXPR   pytest -m gpu -k EXPR                     -> gpurun_out/TAG_pytest_gpu_k.log
+#   smoke        __graft_entry__.smoke()                   -> gpurun_out/TAG_smoke.log
+#   bench        python bench.py (N=1 default line)        -> gpurun_out/TAG_bench.json/.err
+#   bench2       bench.py --gpus 2 --dist-backend gloo (self-launched ranks sharing the GPU)
+#   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
+#   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
+#   clock        PMC clock/CPI passes (gpu_clock.sh)
+#   py:SCRIPT    python tools/SCRIPT (an A/B or probe script) -> gpurun_out/TAG_SCRIPT.log
+TAG=${1:?usage: tools/gpu.sh TAG STEP...}
+shift
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+export TMPDIR=/tmp
+cd "$R" || exit 1
+for step in "$@"; do
+  echo "[gpu.sh] $(date +%T) step $step"
+  case $step in
+    tests)
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$O/${TAG}_pytest_gpu.log" 2>&1 || { tail -30 "$O/${TAG}_pytest_gpu.log"; exit 1; }
+      tail -3 "$O/${TAG}_pytest_gpu.log" ;;
+    tests:*)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${step#tests:}" \
+        > "$O/${TAG}_pytest_gpu_k.log" 2>&1 || { tail -30 "$O/${TAG}_pytest_gpu_k.log"; exit 1; }
+      tail -3 "$O/${TAG}_pytest_gpu_k.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/${TAG}_smoke.log" 2>&1 || exit 1 ;;
+    bench)
+      timeout -k 10 900 python bench.py > "$O/${TAG}_bench.json" 2> "$O/${TAG}_bench.err" || { tail -20 "$O/${TAG}_bench.err"; exit 1; }
+      cat "$O/${TAG}_bench.json" ;;
+    bench2)
+      timeout -k 10 600 python bench.py --gpus 2 --dist-backend gloo --no-cpu --no-configs --no-group \
+        > "$O/${TAG}_bench2_gloo.json" 2> "$O/${TAG}_bench2_gloo.err" || { tail -20 "$O/${TAG}_bench2_gloo.err"; exit 1; }
+      cat "$O/${TAG}_bench2_gloo.json" ;;
+    sim)
+      timeout -k 10 300 python -m flamingo_amd.abides -c flamingo -n 128 -i 1 -p 1 > "$O/${TAG}_sim_c1_n128.log" 2>&1 || exit 1
+      timeout -k 10 600 python -m flamingo_amd.abides -c flamingo -n 1024 -i 2 -p 1 > "$O/${TAG}_sim_n1024_i2.log" 2>&1 || exit 1 ;;
+    prof)
+      bash tools/gpu_prof.sh "$TAG" || exit 1 ;;
+    clock)
+      bash tools/gpu_clock.sh "$TAG" > "$O/${TAG}_clock_run.log" 2>&1 || exit 1 ;;
+    py:*)
+      s=${step#py:}
+      n=${s%.py}
+      timeout -k 10 600 python -u "tools/$s" > "$O/${TAG}_$n.log" 2>&1 || { tail -20 "$O/${TAG}_$n.log"; exit 1; }
+      tail -5 "$O/${TAG}_$n.log" ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] $(date +%T) done"
