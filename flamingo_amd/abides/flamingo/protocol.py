@@ -107,6 +107,18 @@ def server_engine():
     return _group
 
 
+def vector_store(L: int, capacity: int):
+    """The server's device-resident VECTOR store (flamingo_amd.ingest.VectorStore) on
+    server_engine()'s device(s).  An engine object that brings its own store (a test double)
+    provides it through a `vector_store(L, capacity)` method."""
+    eng = server_engine()
+    own = getattr(eng, "vector_store", None)
+    if own is not None:
+        return own(L, capacity)
+    from ...ingest import VectorStore
+    return VectorStore(eng, L, capacity)
+
+
 def committee(num_clients: int) -> set:
     key = (root_seed, committee_size, num_clients)
     if key not in _committees:

@@ -127,10 +127,8 @@ class SA_ServiceAgent(Agent):
 
     # ------------------------------------------------------- device state
     def store(self):
-        from ...ingest import VectorStore
         if self._store is None:
-            self._store = VectorStore(param.server_engine(), self.vector_len, max(1, len(self.users) or
-                                                                                   self.num_clients))
+            self._store = param.vector_store(self.vector_len, max(1, len(self.users) or self.num_clients))
         return self._store
 
     @property
@@ -185,23 +183,19 @@ class SA_ServiceAgent(Agent):
         offline = set(self.users) - online
         # partial sum on the GPU(s) over the rows uploaded at arrival (:346-350); the length guard
         # of :348-349 raises inside partial_sum.  S stays device-resident until reconstruction.
-        import torch
         st = self.store()
         self._accepting = False
         if st.bad:
             raise RuntimeError("Client sends vector of incorrect length.")
         if len(st) != len(self.user_vectors):
             raise RuntimeError("stored vectors do not match the received ones")
-        e0 = torch.cuda.Event(enable_timing=True)
-        e0.record(torch.cuda.current_stream(st.devices[0]))
         t0 = pd.Timestamp("now")
-        done = st.partial_sum()
+        st.partial_sum()
         t1 = pd.Timestamp("now")
-        done.synchronize()
-        self.gpu_ms.setdefault(self.current_iteration, {})["report"] = e0.elapsed_time(done)
+        gpu = st.wait_partial()
+        self.gpu_ms.setdefault(self.current_iteration, {})["report"] = gpu
         self.agent_print(f"report partial sum: host enqueue {(t1 - t0).total_seconds() * 1e3:.3f} ms, "
-                         f"GPU {e0.elapsed_time(done):.3f} ms ({len(st)} rows on {st.G} device(s), uploaded "
-                         "at arrival)")
+                         f"GPU {gpu:.3f} ms ({len(st)} rows on {st.G} device(s), uploaded at arrival)")
         # dropout pairs (online nb, offline id) and their signs (:359-380)
         nbrs = param.neighbors(self.current_iteration, self.num_clients, self.neighborhood_size)
         pairs, signs = P.dropout_pairs(nbrs, online, offline)

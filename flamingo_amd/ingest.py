@@ -108,6 +108,8 @@ class VectorStore:
         import torch
         if self.bad:
             raise RuntimeError("Client sends vector of incorrect length.")
+        self._t0 = torch.cuda.Event(enable_timing=True)
+        self._t0.record(torch.cuda.current_stream(self.devices[0]))
         for r, d in enumerate(self.devices):
             torch.cuda.current_stream(d).wait_stream(self._copy[r])
         if self.group is None:
@@ -135,9 +137,15 @@ class VectorStore:
                 self._consumed[r] = ev
             g.wait()
             self.bounds = [(lo, hi) for lo, hi, _ in sb]
-        self.done = torch.cuda.Event()
+        self.done = torch.cuda.Event(enable_timing=True)
         self.done.record(torch.cuda.current_stream(self.devices[0]))
         return self.done
+
+    def wait_partial(self) -> float:
+        """Block until S is complete; the device time (ms) from partial_sum's call to S done --
+        the uploads still in flight at that call included."""
+        self.done.synchronize()
+        return self._t0.elapsed_time(self.done)
 
     def host_partial(self) -> np.ndarray:
         """S on the host (uint32[L]) -- only for inspection; the round itself never copies it."""

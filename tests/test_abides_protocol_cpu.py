@@ -19,7 +19,45 @@ import oracle as O
 from flamingo_amd import crypto as C
 
 
+class OracleStore:
+    """The server's VECTOR store (flamingo_amd.ingest.VectorStore interface) on the host."""
+
+    def __init__(self, L):
+        self.L, self.G = L, 1
+        self.reset()
+
+    def reset(self):
+        self.rows, self.bad = {}, []
+
+    def __len__(self):
+        return len(self.rows)
+
+    def add(self, sender, vec):
+        v = np.asarray(vec)
+        if v.shape != (self.L,):
+            self.bad.append(sender)
+        else:
+            self.rows[sender] = v.astype(np.uint32)
+
+    def partial_sum(self):
+        rows = np.stack(list(self.rows.values())) if self.rows else np.zeros((0, self.L), np.uint32)
+        self.S = O.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8), L=self.L)
+
+    def wait_partial(self):
+        return 0.0
+
+    def host_partial(self):
+        return self.S
+
+    def unmask(self, seeds, signs):
+        sd = np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32) if seeds else np.zeros((0, 32), np.uint8)
+        return O.aggregate_unmask(self.S[None], sd, np.asarray(signs, np.int8), L=self.L)
+
+
 class OracleEngine:
+    def vector_store(self, L, capacity):
+        return OracleStore(L)
+
     def client_mask(self, seg, seeds, signs, L, x=None):
         return O.client_mask(np.asarray(seg, np.int64), np.frombuffer(b"".join(seeds), np.uint8).reshape(-1, 32),
                              np.asarray(signs, np.int8), L, x=x)
