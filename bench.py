@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL; the real multi-GPU path) or gloo (test only: ranks sharing one GPU)")
     ap.add_argument("--no-group", action="store_true", help="skip the single-process device-group leg")
+    ap.add_argument("--group-leg", action="store_true",
+                    help="internal: run only the device-group leg and print its JSON (bench.py runs it as a child "
+                         "process under a time limit, so a clique that cannot come up cannot hang the bench)")
     ap.add_argument("--group-devices", default="",
                     help="devices of the device-group leg, e.g. 0,0,0,0 (loopback ranks on one GPU); "
                          "default every visible GPU")
@@ -108,8 +111,49 @@ def world_check(gpus: int, world: int, backend: str, devices: int) -> str:
     return ""
 
 
+def group_leg_main(args):
+    """`bench.py --group-leg`: the c4 inputs of main() (same seeds, graph and offline set), then
+    measure_group; prints one JSON object."""
+    import torch
+    from flamingo_amd import params as P
+    N, L = args.total_clients, 1 << args.log2_L
+    cfg = f"c4-n{N}-L{L}"
+    m = np.frombuffer(b"".join(P.bench_seed(cfg, i) for i in range(N)), np.uint8).reshape(N, 32)
+    nbrs = P.neighbor_graph(b"\x00" * 32, 1, N, 1, encrypt=None)
+    g = np.random.Generator(np.random.PCG64(12345))
+    n_off = int(round(args.dropout * N))
+    offline = np.sort(g.choice(N, n_off, replace=False)) if n_off else np.zeros(0, np.int64)
+    online = np.setdiff1d(np.arange(N), offline)
+    sseeds, ssigns = P.server_seed_table(m, nbrs, online, offline, P.synthetic_pair_seed)
+    print(json.dumps(measure_group(torch, P, m, nbrs, online, sseeds, ssigns, L, args.group_devices,
+                                   copy=not args.no_copy)), flush=True)
+    return 0
+
+
+def group_leg_subprocess(args, timeout=240):
+    """The device-group leg in a child process (never an exec: this process has touched the GPU),
+    killed after `timeout` s; a failure or a hang becomes {"error": ...} in the line."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--group-leg", "--total-clients", str(args.total_clients),
+           "--log2-L", str(args.log2_L), "--dropout", str(args.dropout)]
+    if args.group_devices:
+        cmd += ["--group-devices", args.group_devices]
+    if args.no_copy:
+        cmd.append("--no-copy")
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"device-group leg did not finish in {timeout} s (killed)"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"device-group leg exited {r.returncode}: {r.stderr.strip()[-400:]}"}
+    return json.loads(lines[-1])
+
+
 def main():
     args = parse()
+    if args.group_leg:
+        return group_leg_main(args)
     plan = launch_plan(args.gpus, os.environ, sys.argv[1:])
     if plan is not None:
         import subprocess
@@ -332,8 +376,7 @@ def main():
             po = res["variants"]["pairs_only"]
             po["frac_of_practical_peak"] = round(po["GB/s"] / res["roofline"]["practical_peak"]["GB/s"], 4)
         if not args.no_group:
-            res["group"] = measure_group(torch, P, m, nbrs, online, sseeds, ssigns, L, args.group_devices,
-                                         copy=not args.no_copy)
+            res["group"] = group_leg_subprocess(args)
         if not args.no_configs:
             res["other_configs"] = {
                 "c2": measure_config(eng, torch, P, "c2", N=128, L=16384, o=1, dropout=0.0, check_oracle=True),
