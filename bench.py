@@ -853,8 +853,26 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
     rec = ShardedReconstruction(eng, L, comm=comm or ("rccl" if backend == "nccl" else "torch"))
     out = torch.empty(rec.S, dtype=torch.int32, device=dev)
     per_round, oks, Ds = [], True, []
+    rep_ms, fp_ms = [], []
+    S_shard = torch.empty(rec.S, dtype=torch.int32, device=dev)
     cache = {}
     coll = dev if backend == "nccl" else torch.device("cpu")
+
+    def timed(fn):
+        """fn() `steps` times between barriers; max-over-ranks ms per call."""
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()) / steps * 1e3
     for it in range(1, rounds + 1):
         nbrs = P.neighbor_graph(b"\x00" * 32, it, N, 1, encrypt=eng.chacha20_encrypt)
         off = np.sort(np.random.Generator(np.random.PCG64(it)).choice(N, int(round(0.01 * N)), replace=False))
@@ -888,6 +906,11 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         per_round.append(float(el.item()) / steps * 1e3)
         oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
+        # the reference's split: S shards at report time, then shares -> final over them
+        rep_ms.append(timed(lambda: rec.report(rows, S_shard, stream=stream)))
+        out.fill_(0)
+        fp_ms.append(timed(lambda: rec.run_from_partial(S_shard, *args[1:], stream=stream)))
+        oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
         Ds.append(D)
         del rows
     okt = torch.tensor([1 if oks else 0], device=coll)
@@ -897,6 +920,11 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
             "dropout_pairs_D_mean": float(np.mean(Ds)),
             "server_reconstruction_ms": round(ms, 4),
             "GB/s": round((4.0 * (N - round(0.01 * N)) * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
+            "from_report_partial": {"report_rows_to_S_shards_ms": round(float(np.mean(rep_ms)), 4),
+                                    "shares_to_final_ms": round(float(np.mean(fp_ms)), 4),
+                                    "what": "ShardedReconstruction.report (rows -> reduce-scattered S shards, at "
+                                            "report time) and run_from_partial (shares -> final over each rank's "
+                                            "S shard: the all-gather of pair keys is the one exchange)"},
             "correct": bool(okt.item()),
             "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
                         "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "

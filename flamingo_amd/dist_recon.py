@@ -20,6 +20,16 @@ Per rank, in stream order:
 The two exchanges go through the library's RCCL communicator (flm_all_gather_dev,
 flm_reduce_scatter_dev) when one is attached (distributed.init_rccl), else through
 torch.distributed (gloo on host copies: ranks sharing one GPU in tests).
+
+The reference itself splits the round in two steps (report_process :346-350 sums the rows
+before any share exists; reconstruction_process :499-605 adds the masks).  report() +
+run_from_partial() keep that split on G ranks: report reduce-scatters the rows' partial sums
+into each rank's S shard; once the shares arrive, each rank adds every mask over its own S
+shard -- the all-gather of the pair keys is then the only exchange on the shares-to-final
+path, and no row is read there:
+  side:  ec_combine(my pairs) -> chunk -------------------------\
+  main:  shamir(all m_i) -> S shard + self masks -> part ------+-> all_gather(chunk)
+         -> part + pair masks -> out shard
 """
 from __future__ import annotations
 
@@ -129,4 +139,55 @@ class ShardedReconstruction:
         else:
             src = part[0]
         self._reduce_scatter(src, out, main)
+        return out, flags
+
+    # ----------------------------------------------- the reference's two-step split
+    def report(self, rows, S_out, stream=None):
+        """report_process on G ranks: S_out[:S] = this rank's slots of sum over every rank's rows
+        (one rows-only launch over all L, then the reduce-scatter).  rows (N_r, pitch) int32."""
+        main = torch.cuda.current_stream(self.device) if stream is None else stream
+        with torch.cuda.stream(main):
+            part = self._buf("report_part", (self.Lp,), torch.int32, 0)
+        if rows is not None and rows.shape[0]:
+            self.eng.aggregate_unmask_dev(rows, None, None, part, L=self.L, stream=main)
+        else:
+            with torch.cuda.stream(main):
+                part[: self.L].zero_()
+        self._reduce_scatter(part, S_out, main)
+        return S_out
+
+    def run_from_partial(self, S_shard, lambdas, mi_shares, c1_mine, pair_shares_mine, pair_signs, D: int, out,
+                         stream=None):
+        """reconstruction_process on G ranks over the report's S shard (S_shard (>= S,) int32):
+        out[:hi-lo] = S_shard[:hi-lo] + sum of every mask over this rank's slots [lo, hi).
+        Other arguments as run()."""
+        eng = self.eng
+        main = torch.cuda.current_stream(self.device) if stream is None else stream
+        M = mi_shares.shape[1]
+        _, _, Dc = pair_chunk(D, self.world, self.rank)
+        Dr = c1_mine.shape[0] if c1_mine is not None else 0
+        n = self.hi - self.lo
+        with torch.cuda.stream(main):
+            m_seeds = self._buf("m_seeds", (M, 32), torch.uint8)
+            neg = self._buf("neg", (M,), torch.int8, -1)
+            chunk = self._buf("chunk", (max(Dc, 1), 32), torch.uint8, 0)
+            gathered = self._buf("gathered", (max(Dc, 1) * self.world, 32), torch.uint8)
+            flags = self._buf("flags", (max(Dr, 1),), torch.int32)
+            part = self._buf("fp_part", (1, self.S), torch.int32, 0)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        if Dr:
+            self.side.wait_event(ready)
+            eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+        src = S_shard[: self.S].view(1, self.S)
+        if n > 0:
+            eng.aggregate_unmask_dev(src, m_seeds, neg, part[0] if D else out, L=n, prg_slot0=self.lo, stream=main)
+        if D:
+            main.wait_event(done)
+            self._all_gather(chunk, gathered, main)
+            if n > 0:
+                eng.aggregate_unmask_dev(part, gathered[:D], pair_signs, out, L=n, prg_slot0=self.lo, stream=main)
         return out, flags

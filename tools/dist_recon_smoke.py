@@ -57,6 +57,20 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
         good = bool(np.all(got == len(on)))
         print(f"rank {r}/{G} N={N} L={L} D={D} rep {rep}: shard [{rec.lo},{rec.hi}) out==|U| {good}", flush=True)
         ok &= good
+    # the reference's split: S shards at report, masks over them at reconstruction
+    S_shard = torch.full((rec.S,), 5, dtype=torch.int32, device=dev)
+    rec.report(r_rows, S_shard)
+    torch.cuda.synchronize()
+    want_S = rows[torch.from_numpy(on).to(dev)][:, :L].sum(0, dtype=torch.int64).remainder(2**32)
+    got_S = S_shard[: rec.hi - rec.lo].cpu().numpy().view(np.uint32).astype(np.int64)
+    good = bool(np.array_equal(got_S, want_S[rec.lo:rec.hi].cpu().numpy()))
+    out.fill_(7)
+    rec.run_from_partial(S_shard, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]), t(R["pair_shares"][:, a:b]),
+                         t(R["pair_signs"]), D, out)
+    torch.cuda.synchronize()
+    good &= bool(np.all(out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32) == len(on)))
+    print(f"rank {r}/{G} N={N} L={L} D={D} from report partial: S shard and out==|U| {good}", flush=True)
+    ok &= good
 okt = torch.tensor([1 if ok else 0])
 if backend == "nccl":
     okt = okt.to(dev)
