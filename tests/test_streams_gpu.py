@@ -45,7 +45,7 @@ def eng():
     e.close()
 
 
-@pytest.mark.parametrize("N,L", [(64, 16384), (48, 300000)])   # small-round path, items path
+@pytest.mark.parametrize("N,L", [(64, 16384), (48, 600000)])   # small-round path, items path (K*L > 2^26)
 def test_client_mask_dev_does_not_block(eng, N, L):
     import torch
     dev = torch.device("cuda", 0)
