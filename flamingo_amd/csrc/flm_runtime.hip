@@ -214,6 +214,29 @@ StageSlot *stage_acquire(flm_ctx *ctx, size_t bytes, int *rc) {
     return best;
 }
 
+// A few slots made at flm_init, so the first *_dev calls of a context do not pay the pinned and
+// device allocations (c2's client masks: 0.196 ms with a slot allocated in the call, 0.065 ms without).
+constexpr int kStagePrealloc = 4;
+constexpr size_t kStagePreallocBytes = 256u << 10;
+
+void stage_prealloc(flm_ctx *ctx) {
+    for (int i = 0; i < kStagePrealloc; ++i) {
+        auto *s = new StageSlot();
+        if (hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(&s->host, kStagePreallocBytes, hipHostMallocDefault) != hipSuccess ||
+            s->dev.reserve(kStagePreallocBytes) != hipSuccess) {
+            if (s->host) (void)hipHostFree(s->host);
+            s->dev.release();
+            if (s->done) (void)hipEventDestroy(s->done);
+            delete s;
+            (void)hipGetLastError();
+            return;  // the pool fills lazily instead
+        }
+        s->cap = kStagePreallocBytes;
+        ctx->slots.push_back(s);
+    }
+}
+
 // Copy the slot's first `bytes` host bytes to its device buffer on `s`.
 hipError_t stage_upload(StageSlot *slot, size_t bytes, hipStream_t s) {
     return bytes ? hipMemcpyAsync(slot->dev.p, slot->host, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
@@ -879,6 +902,7 @@ int flm_init(flm_ctx **out, int device) {
         delete ctx;
         return fail(nullptr, FLM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    stage_prealloc(ctx);
     *out = ctx;
     return 0;
 }
