@@ -211,10 +211,13 @@ class SA_ServiceAgent(Agent):
         self.labels_and_sig = (labels, C.ecdsa_sign(pki.server_sk, pki.server_pk, labels))
 
     def report_send_message(self):
+        # the pairwise ciphertexts are the same JSON for every committee member: serialised once
+        # (the reference re-serialises them per member inside this loop, :389-401, line 395)
+        pairwise = wire.serialize_dim1_elgamal(self.dec_target_pairwise)
         for cnt, cid in enumerate(sorted(self.user_committee)):
             self.sendMessage(cid, Message({
                 "msg": "SIGN", "sender": self.id, "iteration": self.current_iteration,
-                "dec_target_pairwise": wire.serialize_dim1_elgamal(self.dec_target_pairwise),
+                "dec_target_pairwise": pairwise,
                 "dec_target_mi": wire.serialize_tuples_bytes([self.mi_cipher[c][cnt] for c in self.client_id_list]),
                 "client_id_list": self.client_id_list, "labels": self.labels_and_sig}), tag="comm_dec_server")
 

@@ -18,7 +18,8 @@ import numpy as np
 
 def serialize_dim1_elgamal(elgamal_dict) -> str:
     """{(i, j): (c0, c1)} -> '{"[i, j]": [c0x, c0y, c1x, c1y]}' (util.py:221-228)."""
-    return json.dumps({json.dumps(list(k)): (int(c0[0]), int(c0[1]), int(c1[0]), int(c1[1]))
+    # f"[{i}, {j}]" is json.dumps([i, j]) for int ids, without a dumps call per key
+    return json.dumps({f"[{int(k[0])}, {int(k[1])}]": (int(c0[0]), int(c0[1]), int(c1[0]), int(c1[1]))
                        for k, (c0, c1) in elgamal_dict.items()})
 
 
@@ -46,7 +47,8 @@ def deserialize_dim2_ecp(s: str) -> dict:
 
 def serialize_tuples_bytes(items) -> str:
     """[(ct, nonce), ...] -> '[["hex", "hex"], ...]' (util.py:239-242)."""
-    return json.dumps([(a.hex(), b.hex()) for a, b in items])
+    # the json.dumps text of [[hex, hex], ...], built directly (hex digits need no escaping)
+    return "[" + ", ".join(f'["{a.hex()}", "{b.hex()}"]' for a, b in items) + "]"
 
 
 def deserialize_tuples_bytes(s: str) -> list:
