@@ -7,6 +7,8 @@
 #   smoke        __graft_entry__.smoke()                   -> gpurun_out/TAG_smoke.log
 #   bench        python bench.py (N=1 default line)        -> gpurun_out/TAG_bench.json/.err
 #   bench2       bench.py --gpus 2 --dist-backend gloo (self-launched ranks sharing the GPU)
+#   benchG:N     bench.py --gpus N --dist-backend gloo --steps 3 (N self-launched ranks on the one GPU:
+#                the sharded c4 and c5 paths end to end, correctness only)
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
@@ -38,6 +40,11 @@ for step in "$@"; do
       timeout -k 10 600 python bench.py --gpus 2 --dist-backend gloo --no-cpu --no-configs --no-group \
         > "$O/${TAG}_bench2_gloo.json" 2> "$O/${TAG}_bench2_gloo.err" || { tail -20 "$O/${TAG}_bench2_gloo.err"; exit 1; }
       cat "$O/${TAG}_bench2_gloo.json" ;;
+    benchG:*)
+      n=${step#benchG:}
+      timeout -k 10 900 python bench.py --gpus "$n" --dist-backend gloo --steps 3 --warmup 1 \
+        > "$O/${TAG}_bench_g${n}_gloo.json" 2> "$O/${TAG}_bench_g${n}_gloo.err" || { tail -20 "$O/${TAG}_bench_g${n}_gloo.err"; exit 1; }
+      cut -c1-400 "$O/${TAG}_bench_g${n}_gloo.json" ;;
     sim)
       timeout -k 10 300 python -m flamingo_amd.abides -c flamingo -n 128 -i 1 -p 1 > "$O/${TAG}_sim_c1_n128.log" 2>&1 || exit 1
       timeout -k 10 600 python -m flamingo_amd.abides -c flamingo -n 1024 -i 2 -p 1 > "$O/${TAG}_sim_n1024_i2.log" 2>&1 || exit 1 ;;
