@@ -63,11 +63,11 @@ class VectorStore:
         return len(self._slot)
 
     def add(self, sender, vec):
-        """Store one VECTOR body (uint32[L]); a wrong length is remembered for partial_sum to
-        raise, as report_process does (:348-349)."""
+        """Store one VECTOR body (uint32[L]); a wrong length (or a non-32-bit-integer body) is
+        remembered for partial_sum to raise, as report_process does (:348-349)."""
         import torch
         v = np.asarray(vec)
-        if v.ndim != 1 or v.shape[0] != self.L or v.dtype.itemsize != 4:
+        if v.ndim != 1 or v.shape[0] != self.L or v.dtype.kind not in "ui" or v.dtype.itemsize != 4:
             self.bad.append(sender)
             return
         if sender in self._slot:
@@ -162,7 +162,9 @@ class VectorStore:
         seeds = _seeds_array(seeds)
         signs = _signs_array(signs, seeds.shape[0])
         K = seeds.shape[0]
-        host = torch.empty(self.L, dtype=torch.int32).pin_memory()
+        if getattr(self, "_host_out", None) is None:
+            self._host_out = torch.empty(self.L, dtype=torch.int32).pin_memory()
+        host = self._host_out
         outs = []
         for r, d in enumerate(self.devices):
             lo, hi = self.bounds[r]

@@ -59,6 +59,10 @@ def test_store_rejects_a_wrong_length():
         st.add(2, np.zeros(999, np.uint32))
         with pytest.raises(RuntimeError, match="incorrect length"):
             st.partial_sum()
+        st.reset()
+        st.add(3, np.zeros(1000, np.float32))      # not a uint32 body: never reinterpreted as one
+        with pytest.raises(RuntimeError, match="incorrect length"):
+            st.partial_sum()
 
 
 def test_store_empty_round():
