@@ -62,3 +62,15 @@ def test_world_mismatch_exits_nonzero_before_gpu():
     assert r.returncode == 2, r.stderr[-2000:]
     assert "WORLD_SIZE=2" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_group_leg_failure_becomes_an_error_field():
+    """The device-group leg runs in a child process; when it cannot run (here: no GPU) the bench
+    line gets {"error": ...} instead of the bench failing or hanging."""
+    import argparse
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is visible: the leg would run")
+    args = argparse.Namespace(total_clients=64, log2_L=12, dropout=0.0, group_devices="", no_copy=True)
+    res = bench.group_leg_subprocess(args, timeout=240)
+    assert set(res) == {"error"} and "exited" in res["error"]
