@@ -77,6 +77,16 @@ SIGNATURES = {
     "flm_group_aggregate_unmask_dev": (_int, [_vp, ctypes.POINTER(_vp), _sz, ctypes.POINTER(_int),
                                               ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _sz,
                                               ctypes.POINTER(_vp)]),
+    "flm_store_create": (_int, [ctypes.POINTER(_vp), _vp, _vp, _sz, _int]),
+    "flm_store_free": (None, [_vp]),
+    "flm_store_last_error": (ctypes.c_char_p, [_vp]),
+    "flm_store_count": (_int, [_vp]),
+    "flm_store_add": (_int, [_vp, ctypes.c_int64, _vp, _sz]),
+    "flm_store_partial": (_int, [_vp]),
+    "flm_store_partial_wait": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
+    "flm_store_partial_host": (_int, [_vp, _u32p]),
+    "flm_store_unmask": (_int, [_vp, _u8p, _i8p, _int, _u32p]),
+    "flm_store_reset": (_int, [_vp]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),
 }

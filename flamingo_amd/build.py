@@ -10,7 +10,8 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = [os.path.join(HERE, "csrc", f) for f in ("flm_kernels.hip", "flm_runtime.hip", "flm_p256.hip", "flm_comm.hip")]
+SRC = [os.path.join(HERE, "csrc", f) for f in ("flm_kernels.hip", "flm_runtime.hip", "flm_p256.hip", "flm_comm.hip",
+                                                        "flm_store.hip")]
 HDRS = [os.path.join(HERE, "csrc", "flm_internal.h"),
         os.path.join(os.path.dirname(HERE), "include", "flamingo_hip.h")]
 OUT = os.path.join(HERE, "lib", "libflamingo_hip.so")

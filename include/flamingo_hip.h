@@ -335,6 +335,36 @@ int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, 
                                    const uint8_t *const *d_seeds, const int8_t *const *d_signs, int K, size_t L,
                                    uint32_t *const *d_shards);
 
+/* ------------------------------------------- device-resident VECTOR ingestion */
+
+/* The server's VECTOR bodies on the GPU(s) from arrival to the final sum: the reference keeps
+ * each body in a dict on arrival (SA_ServiceAgent.py:205-210), sums them in report_process
+ * (:346-350) and adds the recovered masks in reconstruction_process (:529-540, :587-605).
+ * flm_store_create: on one context (ctx) or across a group (g; exactly one of them), L slots,
+ *   `capacity` rows expected (the store grows past it).
+ * flm_store_add: copies row[0..n) into pinned staging and returns; the DMA onto the sender's
+ *   device row runs on a copy stream of the store (rows round-robin over the group's devices in
+ *   arrival order; a sender that sends twice overwrites its row, like the reference's dict).
+ *   n != L is remembered and makes flm_store_partial fail with the reference's message (:348-349).
+ * flm_store_partial: enqueues S = sum of the stored rows after their uploads; S stays on the
+ *   device(s) (slot-sharded on a group, after the group's one reduce-scatter).  Returns at once;
+ *   flm_store_partial_wait blocks until S is complete and gives the device time in ms.
+ * flm_store_partial_host: S to the host (inspection only; the round never needs it there).
+ * flm_store_unmask: out[0..L) = S + sum_k signs[k] * PRG(seeds[k]), each device over its own
+ *   slot shard (no exchange), then the one copy to the host; synchronous.
+ * flm_store_reset: forget the rows (the next arrivals wait for the last partial sum's reads). */
+typedef struct flm_store flm_store;
+int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int capacity);
+void flm_store_free(flm_store *st);
+const char *flm_store_last_error(const flm_store *st);
+int flm_store_count(const flm_store *st);
+int flm_store_add(flm_store *st, int64_t sender, const uint32_t *row, size_t n);
+int flm_store_partial(flm_store *st);
+int flm_store_partial_wait(flm_store *st, float *gpu_ms);
+int flm_store_partial_host(flm_store *st, uint32_t *out);
+int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *out);
+int flm_store_reset(flm_store *st);
+
 /* Allocate / free page-locked host memory through HIP (for a pinned arena
  * holding client vectors, so host->device copies are DMA at full PCIe rate). */
 void *flm_host_alloc(size_t bytes);

@@ -35,7 +35,13 @@ for _name, _res, _args in (
         ("flm_ec_combine", _int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint32)]),
         ("flm_group_init", _int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int)]),
         ("flm_group_last_error", ctypes.c_char_p, [_vp]),
-        ("flm_group_aggregate_unmask", _int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p])):
+        ("flm_group_aggregate_unmask", _int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),
+        ("flm_store_create", _int, [ctypes.POINTER(_vp), _vp, _vp, _sz, _int]),
+        ("flm_store_last_error", ctypes.c_char_p, [_vp]),
+        ("flm_store_add", _int, [_vp, ctypes.c_int64, _vp, _sz]),
+        ("flm_store_partial", _int, [_vp]),
+        ("flm_store_unmask", _int, [_vp, _u8p, _i8p, _int, _u32p]),
+        ("flm_store_reset", _int, [_vp])):
     _f = getattr(_lib, _name)
     _f.restype, _f.argtypes = _res, _args
 
@@ -147,3 +153,41 @@ def client_mask(seeds, signs, L, x=None):
     _check(_lib.flm_client_mask(_context(), xp, 1, seg.ctypes.data_as(_i64p), sd.ctypes.data_as(_u8p),
                                 sg.ctypes.data_as(_i8p), L, out.ctypes.data_as(_u32p)))
     return out
+
+
+class VectorStore:
+    """The server's VECTOR bodies on the GPU(s) from arrival to final_sum (flm_store_*): hand each
+    body to add() in receiveMessage (:205-210), call partial() in report_process (:346-350) and
+    unmask() in reconstruction_process (:529-605), reset() when the pools are cleared (:488-497).
+    On FLM_GPUS > 1 devices the rows are spread over the group and S stays slot-sharded."""
+
+    def __init__(self, L, capacity):
+        h = _vp()
+        g = _server_group()
+        if _lib.flm_store_create(ctypes.byref(h), None if g is not None else _context(), g, L, capacity):
+            raise RuntimeError(_lib.flm_store_last_error(None).decode())
+        self.h, self.L = h, L
+
+    def _check(self, rc):
+        if rc:
+            raise RuntimeError(_lib.flm_store_last_error(self.h).decode())
+
+    def add(self, sender, vec):
+        v = np.ascontiguousarray(vec, dtype=np.uint32)
+        self._check(_lib.flm_store_add(self.h, int(sender), v.ctypes.data, v.shape[0]))
+
+    def partial(self):
+        """S = sum of the stored vectors, left on the GPU(s); raises on a body of the wrong length
+        (:348-349)."""
+        self._check(_lib.flm_store_partial(self.h))
+
+    def unmask(self, seeds, signs):
+        """final_sum = S + sum_k signs[k] * PRG(seeds[k]) as uint32[L] (:538-540, :605)."""
+        sd, sg, K = _seed_arrays(seeds, signs)
+        out = np.empty(self.L, np.uint32)
+        self._check(_lib.flm_store_unmask(self.h, sd.ctypes.data_as(_u8p), sg.ctypes.data_as(_i8p), K,
+                                          out.ctypes.data_as(_u32p)))
+        return out
+
+    def reset(self):
+        self._check(_lib.flm_store_reset(self.h))

@@ -39,7 +39,8 @@ def test_store_round_vs_oracle(G, N, K, L):
             for i in order:
                 st.add(int(i), rows[i])
             assert len(st) == N
-            st.partial_sum().synchronize()
+            st.partial_sum()
+            st.wait_partial()
             S = rows.sum(axis=0, dtype=np.uint64).astype(np.uint32)
             assert np.array_equal(st.host_partial(), S)
             got = st.unmask(seeds, signs)
@@ -70,7 +71,33 @@ def test_store_empty_round():
     from flamingo_amd.ingest import VectorStore
     with MaskEngine(0) as eng:
         st = VectorStore(eng, 2048, 4)
-        st.partial_sum().synchronize()
+        st.partial_sum()
+        st.wait_partial()
         assert not st.host_partial().any()
         s = np.arange(32, dtype=np.uint8).reshape(1, 32)
         assert np.array_equal(st.unmask(s, [1]), O.prg(s.tobytes(), 2048))
+
+
+def test_store_c_abi_checks_lengths_and_reset():
+    """The library store itself (flm_store_*, not the Python guard): a body of the wrong length
+    makes flm_store_partial fail with the reference's message; reset clears it; a sender sending
+    twice keeps one row."""
+    import ctypes
+    from flamingo_amd import MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    with MaskEngine(0) as eng:
+        st = VectorStore(eng, 4096, 2)
+        lib = st.lib
+        row = np.arange(4096, dtype=np.uint32)
+        assert lib.flm_store_add(st.h, 7, row.ctypes.data, 4095) == 0        # remembered, not an error yet
+        assert lib.flm_store_partial(st.h) != 0
+        assert b"incorrect length" in lib.flm_store_last_error(st.h)
+        st.reset()
+        for _ in range(2):
+            assert lib.flm_store_add(st.h, 7, row.ctypes.data, 4096) == 0
+        assert lib.flm_store_count(st.h) == 1
+        st.partial_sum()
+        assert st.wait_partial() >= 0.0
+        assert np.array_equal(st.host_partial(), row)
+        assert lib.flm_store_unmask(st.h, None, None, -1, ctypes.cast(row.ctypes.data, ctypes.POINTER(ctypes.c_uint32))) != 0
+        st.close()

@@ -33,7 +33,8 @@ def load_binding(monkeypatch, gpus=None):
 def test_binding_loads_and_binds(monkeypatch):
     flm = load_binding(monkeypatch)
     for name in ("flm_aggregate_unmask", "flm_client_mask", "flm_shamir_combine", "flm_ec_combine",
-                 "flm_group_aggregate_unmask"):
+                 "flm_group_aggregate_unmask", "flm_store_create", "flm_store_add", "flm_store_partial",
+                 "flm_store_unmask", "flm_store_reset"):
         assert getattr(flm._lib, name).argtypes
 
 
@@ -69,3 +70,15 @@ def test_binding_reproduces_reference_round(monkeypatch, ref, refnpz):
     assert b"".join(p_keys) == refnpz[pre + "server_pairs"].tobytes()
     out = flm.aggregate_unmask(rows, m_keys + p_keys, [-1] * len(m_keys) + [r[2] for r in it["recon_symbol"]], L)
     assert digest(out) == it["final_sha256"]
+    # the device-resident form of the same server edit: bodies stored at receiveMessage, S at
+    # report_process, masks added at reconstruction_process
+    st = flm.VectorStore(L, len(rows))
+    for sender, v in zip(it["arrival"], rows):
+        st.add(sender, v)
+    st.partial()
+    out2 = st.unmask(m_keys + p_keys, [-1] * len(m_keys) + [r[2] for r in it["recon_symbol"]])
+    assert digest(out2) == it["final_sha256"]
+    st.reset()
+    st.add(0, rows[0][:-1])
+    with pytest.raises(RuntimeError, match="incorrect length"):
+        st.partial()

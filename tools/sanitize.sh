@@ -13,7 +13,7 @@ mkdir -p build/asan
 hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
   -o build/asan/libflamingo_hip.so flamingo_amd/csrc/flm_kernels.hip flamingo_amd/csrc/flm_runtime.hip \
-  flamingo_amd/csrc/flm_p256.hip flamingo_amd/csrc/flm_comm.hip
+  flamingo_amd/csrc/flm_p256.hip flamingo_amd/csrc/flm_comm.hip flamingo_amd/csrc/flm_store.hip
 
 
 CLANG_RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so 2>/dev/null | head -1)
