@@ -680,6 +680,11 @@ __global__ __launch_bounds__(kEcThreads) void ec_mul_straus_kernel(const uint8_t
 // reconstruction) the per-lane kernel issues fewer instructions.  Exceptional cases as jac_add.
 constexpr int kCoopWaves = 4;
 constexpr int kCoopSlots = 11;
+// FLM_COOP_MODJ (default 1): the kernel carries W = Z^4 (coop_dbl_w / coop_add_w below); 0 builds the
+// plain Jacobian coop_dbl / coop_add for A/B runs
+#ifndef FLM_COOP_MODJ
+#define FLM_COOP_MODJ 1
+#endif
 
 // lane-major slots: a lane's 8 words are 32 contiguous bytes, moved with two 16-byte LDS ops
 // (0.5-1 % faster than word-major single-dword ops, profiles/r02_ab_coop_b128.log)
@@ -697,6 +702,7 @@ __device__ __forceinline__ Fe xget(const uint32_t *slot, int lane) {
     return a;
 }
 
+#if !FLM_COOP_MODJ
 // acc = 2 acc in every wave (all four waves hold acc; wave-uniform branches on w).  The additions
 // of the formula sit off wave 0's last level: L2 gives w1 the multiples of beta, w2 those of
 // gamma^2 and w3 the new Z, so L3 is alpha^2 and alpha (4 beta - X3) with four subtractions.
@@ -866,6 +872,195 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
     acc.Z = xget(F, lane);
 }
 
+#endif  // !FLM_COOP_MODJ
+
+#if FLM_COOP_MODJ
+// ---- modified Jacobian (X, Y, Z, W = Z^4) for the cooperative kernel (FLM_COOP_MODJ, default on)
+// Carrying W takes the doubling's a Z^4 term off the critical path: alpha = 3 (X^2 - W) needs one
+// squaring, so alpha^2 lands one level earlier and a doubling is 3 multiplications of latency and
+// two barriers instead of 4 and three.  Same outputs as dbl-2001-b (X3, Y3, Z3 are identical), so
+// the Jacobian result and everything after it are bit-identical.
+struct JacW {
+    Fe X, Y, Z, W;
+};
+
+//   before barrier 1  w0: XX = X^2, alpha = 3 (XX - W), alpha^2
+//                     w1: beta = X Y^2 -> 4 beta (slot 0), 8 beta (slot 1)
+//                     w2: gamma^2 -> 8 gamma^2 (slot 2)            w3: Z3 = 2 Y Z
+//   between barriers  w0: X3 = alpha^2 - 8 beta, Y3 = alpha (4 beta - X3) - 8 gamma^2 (slots 6, 7)
+//                     w2: W3 = 16 gamma^2 W (slot 9)                w3: Z3 (slot 8)
+// Slots 0..2 are read by w0 before barrier 2; the results (6..9) are written only between the two
+// barriers, so the next operation's writes before its first barrier (slots 0..2 for a doubling,
+// A/B = 0/1 for an addition) never land on a slot another wave is still reading.
+__device__ __forceinline__ void coop_dbl_w(JacW &acc, int w, int lane, uint32_t *S) {
+    Fe alpha, a2, g8, z3;
+    if (w == 0) {
+        const Fe t = fe_sub(fe_sqr(acc.X), acc.W);
+        alpha = fe_add(fe_add(t, t), t);
+        a2 = fe_sqr(alpha);
+    } else if (w == 1) {
+        const Fe beta = fe_mul(acc.X, fe_sqr(acc.Y));
+        const Fe b2 = fe_add(beta, beta);
+        const Fe b4 = fe_add(b2, b2);
+        xput(S + 0 * 512, b4, lane);
+        xput(S + 1 * 512, fe_add(b4, b4), lane);
+    } else if (w == 2) {
+        Fe g = fe_sqr(fe_sqr(acc.Y));
+        g = fe_add(g, g);
+        g = fe_add(g, g);
+        g8 = fe_add(g, g);
+        xput(S + 2 * 512, g8, lane);
+    } else {
+        const Fe yz = fe_mul(acc.Y, acc.Z);
+        z3 = fe_add(yz, yz);
+    }
+    __syncthreads();
+    if (w == 0) {
+        const Fe x3 = fe_sub(a2, xget(S + 1 * 512, lane));
+        xput(S + 6 * 512, x3, lane);
+        xput(S + 7 * 512, fe_sub(fe_mul(alpha, fe_sub(xget(S + 0 * 512, lane), x3)), xget(S + 2 * 512, lane)), lane);
+    } else if (w == 2) {
+        xput(S + 9 * 512, fe_mul(fe_add(g8, g8), acc.W), lane);
+    } else if (w == 3) {
+        xput(S + 8 * 512, z3, lane);
+    }
+    __syncthreads();
+    acc.X = xget(S + 6 * 512, lane);
+    acc.Y = xget(S + 7 * 512, lane);
+    acc.Z = xget(S + 8 * 512, lane);
+    acc.W = xget(S + 9 * 512, lane);
+}
+
+// coop_add with W carried: the same six levels; w3, idle after L3, squares its Z3 twice (L4, L5)
+// into slot H, and L6 picks W for the exceptional cases (Q or a doubling: two squarings of the new
+// Z on that rare path; infinity: 0; acc: its own W).  Result slots D, E, F and K (W).
+__device__ __forceinline__ void coop_add_w(JacW &acc, bool sel, int tab_idx, bool neg, int w, int lane, uint32_t *S,
+                                           const uint32_t *tab) {
+    const uint32_t *q = tab + (size_t)tab_idx * 24 * 64;
+    Jac Q;
+    Q.X = xget(q, lane);
+    Q.Y = xget(q + 8 * 64, lane);
+    Q.Z = xget(q + 16 * 64, lane);
+    if (neg) Q.Y = fe_neg(Q.Y);
+    uint32_t *A = S, *B = S + 512, *C = S + 2 * 512, *Dd = S + 3 * 512, *E = S + 4 * 512, *F = S + 5 * 512,
+             *G = S + 6 * 512, *H = S + 7 * 512, *I = S + 8 * 512, *J = S + 9 * 512, *K = S + 10 * 512;
+    Fe z1z1, z2z2, zz, s2a, s1a, u1, u2, s2, s1, h, i, j, v, x3, y3a, z3;
+    // L1
+    if (w == 0) {
+        z1z1 = fe_sqr(acc.Z);
+        xput(A, z1z1, lane);
+    } else if (w == 1) {
+        z2z2 = fe_sqr(Q.Z);
+        xput(B, z2z2, lane);
+    } else if (w == 2) {
+        zz = fe_sqr(fe_add(acc.Z, Q.Z));
+    } else {
+        s1a = fe_mul(acc.Y, Q.Z);
+    }
+    __syncthreads();
+    // L2
+    if (w == 0) {
+        xput(Dd, fe_mul(Q.X, z1z1), lane);  // u2
+    } else if (w == 1) {
+        u1 = fe_mul(acc.X, z2z2);
+        xput(E, u1, lane);
+    } else if (w == 2) {
+        z1z1 = xget(A, lane);
+        z2z2 = xget(B, lane);
+        xput(F, fe_sub(fe_sub(zz, z1z1), z2z2), lane);  // Z3'
+        s2a = fe_mul(Q.Y, acc.Z);
+    } else {
+        z2z2 = xget(B, lane);
+        xput(G, fe_mul(s1a, z2z2), lane);  // s1
+    }
+    __syncthreads();
+    // L3
+    if (w == 0) {
+        u2 = xget(Dd, lane);
+        u1 = xget(E, lane);
+        h = fe_sub(u2, u1);
+        const Fe h2 = fe_add(h, h);
+        i = fe_sqr(h2);
+        xput(H, i, lane);
+    } else if (w == 2) {
+        s2 = fe_mul(s2a, z1z1);
+    } else if (w == 3) {
+        u2 = xget(Dd, lane);
+        u1 = xget(E, lane);
+        z3 = fe_mul(xget(F, lane), fe_sub(u2, u1));  // Z3 = Z3' h
+        xput(I, z3, lane);
+    }
+    __syncthreads();
+    // L4
+    if (w == 0) {
+        j = fe_mul(h, i);
+        xput(J, j, lane);
+    } else if (w == 1) {
+        i = xget(H, lane);
+        v = fe_mul(u1, i);
+        xput(K, v, lane);
+        xput(Dd, fe_add(v, v), lane);
+    } else if (w == 2) {
+        s1 = xget(G, lane);
+        Fe r = fe_sub(s2, s1);
+        r = fe_add(r, r);
+        xput(A, r, lane);
+        xput(B, fe_sqr(r), lane);
+    } else {
+        z3 = fe_sqr(z3);
+    }
+    __syncthreads();
+    // L5
+    Fe r;
+    if (w == 0) {
+        v = xget(K, lane);
+        r = xget(A, lane);
+        const Fe rr = xget(B, lane);
+        x3 = fe_sub(fe_sub(rr, j), xget(Dd, lane));
+        y3a = fe_mul(r, fe_sub(v, x3));
+    } else if (w == 1) {
+        s1 = xget(G, lane);
+        j = xget(J, lane);
+        const Fe s1j = fe_mul(s1, j);
+        xput(C, fe_add(s1j, s1j), lane);
+    } else if (w == 3) {
+        xput(H, fe_sqr(z3), lane);  // W3 = Z3^4 (H's i was read at L4)
+    }
+    __syncthreads();
+    // L6
+    if (w == 0) {
+        JacW R;
+        R.X = x3;
+        R.Y = fe_sub(y3a, xget(C, lane));
+        R.Z = xget(I, lane);
+        R.W = xget(H, lane);
+        if (fe_is_zero(acc.Z)) {
+            R.X = Q.X; R.Y = Q.Y; R.Z = Q.Z;
+            R.W = fe_sqr(fe_sqr(Q.Z));
+        } else if (fe_is_zero(Q.Z)) {
+            R = acc;
+        } else if (fe_is_zero(h)) {
+            Jac a;
+            a.X = acc.X; a.Y = acc.Y; a.Z = acc.Z;
+            const Jac d = fe_is_zero(r) ? jac_dbl(a) : jac_inf();  // acc == Q / acc == -Q (rare: one lane)
+            R.X = d.X; R.Y = d.Y; R.Z = d.Z;
+            R.W = fe_sqr(fe_sqr(d.Z));
+        }
+        if (!sel) R = acc;
+        xput(Dd, R.X, lane);
+        xput(E, R.Y, lane);
+        xput(F, R.Z, lane);
+        xput(K, R.W, lane);
+    }
+    __syncthreads();
+    acc.X = xget(Dd, lane);
+    acc.Y = xget(E, lane);
+    acc.Z = xget(F, lane);
+    acc.W = xget(K, lane);
+}
+
+#endif  // FLM_COOP_MODJ
+
 __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint8_t *__restrict__ points,
                                                                    const uint8_t *__restrict__ scalars,
                                                                    int per_element, int T, int D,
@@ -892,6 +1087,60 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
         for (int k = 0; k < kNafLen; ++k) dig[k] = 0;
     }
     if (w == 0 && valid && !ok) atomicOr(&flags[i], 2u);
+#if FLM_COOP_MODJ
+    // table of odd multiples (2k+1) P (X, Y, Z only: an addend's W is needed on the rare path only)
+    JacW PW;
+    PW.X = P.X; PW.Y = P.Y; PW.Z = P.Z;
+    PW.W = fe_sqr(fe_sqr(P.Z));
+    JacW P2 = PW;
+    coop_dbl_w(P2, w, lane, S);
+    if (w == 0) {
+        xput(tab, P.X, lane);
+        xput(tab + 8 * 64, P.Y, lane);
+        xput(tab + 16 * 64, P.Z, lane);
+        xput(tab + 24 * 64, P2.X, lane);
+        xput(tab + 32 * 64, P2.Y, lane);
+        xput(tab + 40 * 64, P2.Z, lane);
+    }
+    __syncthreads();
+    JacW t = PW;
+#pragma unroll 1
+    for (int k = 1; k < 8; ++k) {
+        coop_add_w(t, true, 1, false, w, lane, S, tab);
+        if (w == 0) {
+            uint32_t *q = tab + (size_t)(k == 1 ? 8 : k) * 24 * 64;
+            xput(q, t.X, lane);
+            xput(q + 8 * 64, t.Y, lane);
+            xput(q + 16 * 64, t.Z, lane);
+        }
+        __syncthreads();
+    }
+    if (w == 0) {
+        const uint32_t *q = tab + (size_t)8 * 24 * 64;
+        xput(tab + 24 * 64, xget(q, lane), lane);
+        xput(tab + 32 * 64, xget(q + 8 * 64, lane), lane);
+        xput(tab + 40 * 64, xget(q + 16 * 64, lane), lane);
+    }
+    __syncthreads();
+    JacW accw;
+    {
+        const Jac inf = jac_inf();
+        accw.X = inf.X; accw.Y = inf.Y; accw.Z = inf.Z;
+        accw.W = inf.Z;  // 0
+    }
+#pragma unroll 1
+    for (int k = kNafLen - 1; k >= 0; --k) {
+        coop_dbl_w(accw, w, lane, S);
+        const int v = dig[k];
+        if (__any(v != 0)) coop_add_w(accw, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab);
+    }
+    if (w == 0 && valid) {
+        Jac acc;
+        acc.X = accw.X; acc.Y = accw.Y; acc.Z = accw.Z;
+        if (!ok) acc = jac_inf();
+        store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
+    }
+#else
     // table of odd multiples (2k+1) P: 2P into entry 1 as the addend, then entry k = entry k-1 + 2P
     Jac P2 = P;
     coop_dbl(P2, w, lane, S);
@@ -934,6 +1183,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
         if (!ok) acc = jac_inf();
         store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
     }
+#endif
 }
 
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};

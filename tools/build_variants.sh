@@ -9,7 +9,7 @@ O=/tmp/flm_var_objs
 V=${VAR_SRC:-flm_kernels}
 mkdir -p $O
 others=()
-for f in flm_kernels flm_runtime flm_p256 flm_comm; do
+for f in flm_kernels flm_runtime flm_p256 flm_comm flm_store; do
   [ $f = $V ] && continue
   others+=($O/$f.o)
   if [ ! $O/$f.o -nt $C/$f.hip ] || [ ! $O/$f.o -nt $C/flm_internal.h ]; then
