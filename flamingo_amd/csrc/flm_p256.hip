@@ -74,52 +74,40 @@ __device__ __forceinline__ bool fe_lt_p(const Fe &a) {
     return b != 0;
 }
 
+// Carry chains go through __builtin_addc / __builtin_subc, which lower to v_add_co / v_addc_co
+// (v_sub_co / v_subb_co) with the carry in VCC: 8 instructions per 256-bit add.  The earlier
+// 64-bit C form compiled to 64-bit shift-adds plus register moves: fe_add 95 VALU -> 28, fe_sub
+// 75 -> 24 (gfx950 ISA count); a lone wave of the EC chain issues one VALU per ~8 cycles, so the
+// instruction count is its latency.
 // r = (t8:t) - p if that does not borrow (or t8 set), else t; requires t < 2p
 __device__ __forceinline__ void fe_reduce_once(Fe &r, const uint32_t (&t)[8], uint32_t t8) {
-    uint32_t d[8];
-    uint64_t b = 0;
+    uint32_t d[8], b = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t x = (uint64_t)t[i] - kP[i] - b;
-        d[i] = (uint32_t)x;
-        b = x >> 63;
-    }
-    bool take = t8 || !b;
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_subc(t[i], kP[i], b, &b);
+    const bool take = t8 || !b;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = take ? d[i] : t[i];
 }
 
 __device__ __forceinline__ Fe fe_add(const Fe &a, const Fe &b) {
-    uint32_t s[8];
-    uint64_t c = 0;
+    uint32_t s[8], c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c = (uint64_t)a.v[i] + b.v[i] + (c >> 32);
-        s[i] = (uint32_t)c;
-    }
+    for (int i = 0; i < 8; ++i) s[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
     Fe r;
-    fe_reduce_once(r, s, (uint32_t)(c >> 32));
+    fe_reduce_once(r, s, c);
     return r;
 }
 
 __device__ __forceinline__ Fe fe_sub(const Fe &a, const Fe &b) {
-    uint32_t d[8];
-    uint64_t br = 0;
+    uint32_t d[8], br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t x = (uint64_t)a.v[i] - b.v[i] - br;
-        d[i] = (uint32_t)x;
-        br = x >> 63;
-    }
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
     // borrow -> add p back (mask instead of branch)
-    uint32_t m = 0u - (uint32_t)br;
+    const uint32_t m = 0u - br;
     Fe r;
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c = (uint64_t)d[i] + (kP[i] & m) + (c >> 32);
-        r.v[i] = (uint32_t)c;
-    }
+    for (int i = 0; i < 8; ++i) r.v[i] = __builtin_addc(d[i], kP[i] & m, c, &c);
     return r;
 }
 
@@ -155,37 +143,58 @@ __device__ __forceinline__ Fe mont_reduce(uint32_t (&t)[16]) {
 // (tools/ec_probe.hip); one statement per column drops most of the remaining pads.
 #define FLM_MC(n) "v_mad_u64_u32 %[acc], %[c], %[a" #n "], %[b" #n "], %[acc]\n\t" \
                   "v_addc_co_u32_e64 %[hi], %[c], 0, %[hi], %[c]\n\t"
+// first product of a column whose carry counter starts at zero: hi = carry, written fresh (no
+// zeroing move before the statement)
+#define FLM_MC_H "v_mad_u64_u32 %[acc], %[c], %[a0], %[b0], %[acc]\n\t" \
+                 "v_addc_co_u32_e64 %[hi], %[c], 0, 0, %[c]\n\t"
+// first product of a column whose accumulator starts at zero: acc = a*b (cannot carry), hi = 0
+#define FLM_MC_Z "v_mad_u64_u32 %[acc], %[c], %[a0], %[b0], 0\n\t" \
+                 "v_mov_b32 %[hi], 0\n\t"
+#define FLM_R1
+#define FLM_R2 FLM_R1 FLM_MC(1)
+#define FLM_R3 FLM_R2 FLM_MC(2)
+#define FLM_R4 FLM_R3 FLM_MC(3)
+#define FLM_R5 FLM_R4 FLM_MC(4)
+#define FLM_R6 FLM_R5 FLM_MC(5)
+#define FLM_R7 FLM_R6 FLM_MC(6)
+#define FLM_R8 FLM_R7 FLM_MC(7)
 #define FLM_MI(n) [a##n] "v"(a[n]), [b##n] "v"(b[n])
-#define FLM_MO(n) , FLM_MI(n)
+#define FLM_I1 FLM_MI(0)
+#define FLM_I2 FLM_I1, FLM_MI(1)
+#define FLM_I3 FLM_I2, FLM_MI(2)
+#define FLM_I4 FLM_I3, FLM_MI(3)
+#define FLM_I5 FLM_I4, FLM_MI(4)
+#define FLM_I6 FLM_I5, FLM_MI(5)
+#define FLM_I7 FLM_I6, FLM_MI(6)
+#define FLM_I8 FLM_I7, FLM_MI(7)
 // acc/hi are early-clobber: later products read inputs after the first mad/addc wrote them,
 // so no input may share their registers (the compiler otherwise reuses one holding the same
 // value, e.g. a zero limb of the constant 1 against hi's initial 0)
-#define FLM_MOUT [acc] "+&v"(acc), [hi] "+&v"(hi), [c] "=&s"(c)
-template <int NP>
+#define FLM_MOUT0 [acc] "+&v"(acc), [hi] "+&v"(hi), [c] "=&s"(c)
+#define FLM_MOUT1 [acc] "+&v"(acc), [hi] "=&v"(hi), [c] "=&s"(c)
+#define FLM_MOUT2 [acc] "=&v"(acc), [hi] "=&v"(hi), [c] "=&s"(c)
+#define FLM_MCASE(N)                                                                \
+    if constexpr (NP == N) {                                                        \
+        if constexpr (MODE == 0) asm(FLM_MC(0) FLM_R##N : FLM_MOUT0 : FLM_I##N);    \
+        else if constexpr (MODE == 1) asm(FLM_MC_H FLM_R##N : FLM_MOUT1 : FLM_I##N); \
+        else asm(FLM_MC_Z FLM_R##N : FLM_MOUT2 : FLM_I##N);                          \
+    }
+// MODE 0: acc and hi carry in; 1: acc carries in, hi starts at zero; 2: both start at zero
+// (modes 1/2 write the fresh words in the statement instead of zeroing registers before it:
+// the per-column moves were ~45 of fe_mul's VALU instructions)
+template <int NP, int MODE = 0>
 __device__ __forceinline__ void mad_col(uint64_t &acc, uint32_t &hi, const uint32_t (&a)[NP], const uint32_t (&b)[NP]) {
     uint64_t c;
-    if constexpr (NP == 1) asm(FLM_MC(0) : FLM_MOUT : FLM_MI(0));
-    else if constexpr (NP == 2) asm(FLM_MC(0) FLM_MC(1) : FLM_MOUT : FLM_MI(0) FLM_MO(1));
-    else if constexpr (NP == 3) asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2));
-    else if constexpr (NP == 4)
-        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3));
-    else if constexpr (NP == 5)
-        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4)
-            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4));
-    else if constexpr (NP == 6)
-        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5)
-            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5));
-    else if constexpr (NP == 7)
-        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5) FLM_MC(6)
-            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5) FLM_MO(6));
-    else
-        asm(FLM_MC(0) FLM_MC(1) FLM_MC(2) FLM_MC(3) FLM_MC(4) FLM_MC(5) FLM_MC(6) FLM_MC(7)
-            : FLM_MOUT : FLM_MI(0) FLM_MO(1) FLM_MO(2) FLM_MO(3) FLM_MO(4) FLM_MO(5) FLM_MO(6) FLM_MO(7));
+    FLM_MCASE(1) FLM_MCASE(2) FLM_MCASE(3) FLM_MCASE(4) FLM_MCASE(5) FLM_MCASE(6) FLM_MCASE(7) FLM_MCASE(8)
 }
+#undef FLM_MCASE
 #undef FLM_MC
-#undef FLM_MO
+#undef FLM_MC_H
+#undef FLM_MC_Z
 #undef FLM_MI
-#undef FLM_MOUT
+#undef FLM_MOUT0
+#undef FLM_MOUT1
+#undef FLM_MOUT2
 
 // column K of a*b (products a_i b_{K-i}) into acc/hi
 template <int K>
@@ -197,7 +206,7 @@ __device__ __forceinline__ void mul_col(uint64_t &acc, uint32_t &hi, const Fe &a
         av[q] = a.v[lo + q];
         bv[q] = b.v[K - lo - q];
     }
-    mad_col<n>(acc, hi, av, bv);
+    mad_col<n, K == 0 ? 2 : 1>(acc, hi, av, bv);  // hi (and at K = 0 acc) start at zero
 }
 
 // column K of the doubled cross products of a^2 (a_i a_j, i < j, i + j = K)
@@ -211,7 +220,10 @@ __device__ __forceinline__ void sqr_col(uint64_t &x, uint32_t &xh, const Fe &a) 
             av[q] = a.v[lo + q];
             bv[q] = a.v[K - lo - q];
         }
-        mad_col<n>(x, xh, av, bv);
+        mad_col<n, 2>(x, xh, av, bv);  // x and xh start at zero
+    } else {
+        x = 0;
+        xh = 0;
     }
 }
 
@@ -221,7 +233,6 @@ __device__ __forceinline__ void mul_cols(uint64_t &acc, uint32_t &hi, uint32_t (
         mul_col<K>(acc, hi, a, b);
         t[K] = (uint32_t)acc;
         acc = (acc >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
         mul_cols<K + 1>(acc, hi, t, a, b);
     }
 }
@@ -229,8 +240,8 @@ __device__ __forceinline__ void mul_cols(uint64_t &acc, uint32_t &hi, uint32_t (
 // Montgomery product a*b*R^-1 mod p: product scanning with a 96-bit column accumulator
 __device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
     uint32_t t[16];
-    uint64_t acc = 0;
-    uint32_t hi = 0;
+    uint64_t acc;  // written by column 0
+    uint32_t hi;
     mul_cols<0>(acc, hi, t, a, b);
     t[15] = (uint32_t)acc;
     return mont_reduce(t);
@@ -239,8 +250,8 @@ __device__ __forceinline__ Fe fe_mul(const Fe &a, const Fe &b) {
 template <int K>
 __device__ __forceinline__ void sqr_cols(uint64_t &c, uint32_t (&t)[16], const Fe &a) {
     if constexpr (K < 15) {
-        uint64_t x = 0;
-        uint32_t xh = 0;
+        uint64_t x;
+        uint32_t xh;
         sqr_col<K>(x, xh, a);
         xh = (xh << 1) | (uint32_t)(x >> 63);
         x <<= 1;
@@ -1259,15 +1270,10 @@ __device__ constexpr uint32_t kR2N[8] = {0xbe79eea2u, 0x83244c95u, 0x49bd6fa6u, 
 constexpr uint32_t kN0 = 0xee00bc4fu;                                                             // -n^-1 mod 2^32
 
 __device__ __forceinline__ void sc_reduce_once(Fe &r, const uint32_t (&t)[8], uint32_t t8) {
-    uint32_t d[8];
-    uint64_t b = 0;
+    uint32_t d[8], b = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t x = (uint64_t)t[i] - kN[i] - b;
-        d[i] = (uint32_t)x;
-        b = x >> 63;
-    }
-    bool take = t8 || !b;
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_subc(t[i], kN[i], b, &b);
+    const bool take = t8 || !b;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = take ? d[i] : t[i];
 }
@@ -1302,15 +1308,11 @@ __device__ __forceinline__ Fe sc_mul(const Fe &a, const Fe &b) {
 }
 
 __device__ __forceinline__ Fe sc_add(const Fe &a, const Fe &b) {
-    uint32_t s[8];
-    uint64_t c = 0;
+    uint32_t s[8], c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c = (uint64_t)a.v[i] + b.v[i] + (c >> 32);
-        s[i] = (uint32_t)c;
-    }
+    for (int i = 0; i < 8; ++i) s[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
     Fe r;
-    sc_reduce_once(r, s, (uint32_t)(c >> 32));
+    sc_reduce_once(r, s, c);
     return r;
 }
 

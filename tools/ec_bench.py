@@ -24,7 +24,8 @@ ap.add_argument("--T", type=int, default=20)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--cpu-sample", type=int, default=100, help="scalar mults timed on the host")
 ap.add_argument("--threads", type=int, default=64)
-ap.add_argument("--scalars", choices=["random", "lagrange"], default="random")
+ap.add_argument("--scalars", choices=["random", "lagrange", "pow2"], default="random",
+                help="pow2: every lambda = 2^255 (one wNAF digit: ~258 doublings and no additions, to split the chain)")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
 ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
 ap.add_argument("--spread", type=int, default=0, help="flm_set_tuning ec_spread (KiB of LDS per EC workgroup)")
@@ -38,6 +39,8 @@ shares = np.stack([C.points_to_wire([base[(j * 7 + i) % 64] for i in range(a.D)]
 if a.scalars == "lagrange":
     from flamingo_amd.abides.flamingo.seeds import lagrange_at_zero
     lams = lagrange_at_zero(sorted(rng.sample(range(1, 61), a.T)))
+elif a.scalars == "pow2":
+    lams = [1 << 255] * a.T
 else:
     lams = [rng.randrange(1, C.N) for _ in range(a.T)]
 c1 = C.points_to_wire([base[(i * 3) % 64] for i in range(a.D)])
