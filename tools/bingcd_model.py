@@ -37,12 +37,20 @@ def inv(x, outer=18, trace=None):
     assert a == 0 and b == 1, (x, a, b)
     return v
 
-rng = random.Random(5)
-cases = [1, 2, 3, P - 1, P - 2, 2**255, 2**224, 2**96 - 1, (P - 1) // 2, 2**64 - 1, 2**30 + 1] + [rng.randrange(1, P) for _ in range(20000)]
-worst = 0
-for x in cases:
-    tr = {}
-    r = inv(x, trace=tr)
-    assert r == pow(x, P - 2, P), x
-    worst = max(worst, tr['done'])
-print("ok", len(cases), "worst outer iterations to a == 0:", worst)
+def check(n_random=20000, seed=5):
+    """Every input converges within the 18 outer steps and matches Fermat; returns the worst
+    number of outer steps any input needed."""
+    rng = random.Random(seed)
+    cases = [1, 2, 3, P - 1, P - 2, 2**255, 2**224, 2**96 - 1, (P - 1) // 2, 2**64 - 1, 2**30 + 1] + [rng.randrange(1, P) for _ in range(n_random)]
+    worst = 0
+    for x in cases:
+        tr = {}
+        r = inv(x, trace=tr)
+        assert r == pow(x, P - 2, P), x
+        worst = max(worst, tr['done'])
+    return len(cases), worst
+
+
+if __name__ == "__main__":
+    n, worst = check()
+    print("ok", n, "worst outer iterations to a == 0:", worst)
