@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--dropout", type=float, default=0.0, help="fraction of clients offline (c5: 0.01)")
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed rounds before the warm-up until this much GPU time has passed: MI355X ramps its "
-                         "clock over ~100 ms of load (tools/tail_probe.py, DESIGN.md section 6)")
+                         "clock over ~100 ms of load (tools/probes/tail_probe.py, DESIGN.md section 6)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-copy", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")

@@ -280,7 +280,7 @@ int grow(flm_group *g, int r, uint32_t *&p, size_t &cap, size_t words) {
     hipError_t e = hipMalloc(&p, std::max<size_t>(words, 64) * sizeof(uint32_t));
     // zeroed on the rank's own stream, ahead of the round that writes it: a plain hipMemset is
     // enqueued on the null stream, which the non-blocking rank streams do not wait for, so it
-    // could land after the round behind the caller's earlier work (tools/group_order_probe.py)
+    // could land after the round behind the caller's earlier work (tools/probes/group_order_probe.py)
     if (e == hipSuccess)
         e = hipMemsetAsync(p, 0, std::max<size_t>(words, 64) * sizeof(uint32_t), flm::rt::stream_of(g->ctx[r]));
     if (e != hipSuccess) return gfail(g, FLM_ENOMEM, std::string("group buffer: ") + hipGetErrorString(e));

@@ -44,7 +44,7 @@ namespace flm {
 // ...), and an s_nop after every rotate.  gfx950 issues v_add_u32 / v_xor_b32 in about 2 cycles
 // and the v_alignbit_b32 rotate in about 4 (profiles/r01_isa_probe3.log); a wave that issues a
 // rotate right behind another rotate, or right before the add that reads it, holds up the SIMD
-// for the other waves.  Measured on the c4 mask-only launch (tools/ab_variants.sh,
+// for the other waves.  Measured on the c4 mask-only launch (tools/ab/ab_variants.sh,
 // profiles/r02_ab_nops.log; 1024 seeds x 2^20 slots, 8 waves/SIMD):
 //   one asm statement per instruction (round 1: the compiler then pads each statement boundary
 //   where the next reads what the previous wrote with an s_nop 0, i.e. after every group of 4)  1.426 ms
@@ -54,7 +54,7 @@ namespace flm {
 //   one statement, s_nop 1 after each of the first three rotates, s_nop 2 after the fourth,
 //   nothing between the adds and xors (FLM_GAP_* defaults below)                                 1.176
 // Gaps between simple ops cost time; gaps after rotates buy it.  The gap macros stay
-// overridable (-DFLM_GAP_...) for tools/build_variants.sh.
+// overridable (-DFLM_GAP_...) for tools/ab/build_variants.sh.
 #ifndef FLM_GAP_A1
 #define FLM_GAP_A1 ""  // between the 2nd and 3rd add of a step
 #endif
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         // when there is one.  With a static split (64 seeds per wave at c4) the SIMD's arbiter
         // lets some waves run far ahead, and a workgroup waited at its barrier for its slowest
         // wave: 0.33-0.62 ms workgroup times, wave 0 idle ~0.2 ms of them, 87 % mean residency
-        // (tools/wg_trace.py, profiles/r02_wg_trace.log).  Claiming, a fast wave takes more
+        // (tools/probes/wg_trace.py, profiles/r02_wg_trace.log).  Claiming, a fast wave takes more
         // units and the waves of a workgroup finish within about one block of each other.
         // Any split gives the same bits: the partials are summed mod 2^32.
         const uint32_t NR = (has_rows && row_valid > 0) ? it.nrows : 0u;

@@ -140,7 +140,7 @@ __device__ __forceinline__ Fe mont_reduce(uint32_t (&t)[16]) {
 // feeds one v_addc).  The compiler pads each inline-asm boundary with s_nop (it cannot see
 // through asm): one statement per product pair measured 543 ns per single-wave multiply,
 // against 669 ns with mad and addc in separate statements and 860 ns for a plain 64-bit C CIOS
-// (tools/ec_probe.hip); one statement per column drops most of the remaining pads.
+// (tools/probes/ec_probe.hip); one statement per column drops most of the remaining pads.
 #define FLM_MC(n) "v_mad_u64_u32 %[acc], %[c], %[a" #n "], %[b" #n "], %[acc]\n\t" \
                   "v_addc_co_u32_e64 %[hi], %[c], 0, %[hi], %[c]\n\t"
 // first product of a column whose carry counter starts at zero: hi = carry, written fresh (no

@@ -384,7 +384,7 @@ int choose_parts(uint64_t tiles_r, uint64_t tiles_m, uint32_t nrows, uint32_t ns
 
 int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     int v = ctx->tune_variant;
-    // measured (tools/ab_items.py, profiles/r01_ab_items*.log): merged accumulator
+    // measured (tools/ab/ab_items.py, profiles/r01_ab_items*.log): merged accumulator
     // fastest where legal (seeds spread over the rows when seed-light), block next
     if (v < 0)
         v = plan.single_tile ? (plan.seed_light ? flm::kVarMergedSpread : flm::kVarMerged)
@@ -682,7 +682,7 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
     if (!pinned.empty()) {
         // Page-locked rows go straight to the device, spread over kCopyStreams
         // streams (several SDMA engines: one stream tops out near 49 GB/s, four
-        // reach the link's ~57 GB/s, tools/h2d_probe.hip).  Runs of rows that are
+        // reach the link's ~57 GB/s, tools/probes/h2d_probe.hip).  Runs of rows that are
         // contiguous on the host (an arena) move as one copy of up to 16 rows.
         if (!ctx->copy[0]) {
             for (int c = 0; c < kCopyStreams; ++c) {
