@@ -198,7 +198,8 @@ int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128
     Rccl *r = rccl();
     if (!r) return rccl_missing(ctx);
     flm::comm_release(ctx);
-    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    flm::rt::DeviceScope dev_scope_;
+    FLM_HIPC(ctx, dev_scope_.set(flm::rt::device_of(ctx)));
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof uid);
     auto *cs = new CommState();
@@ -226,7 +227,8 @@ int flm_reduce_scatter_dev(flm_ctx *ctx, const uint32_t *d_send, uint32_t *d_rec
     CommState *cs = comm_of(ctx);
     if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
     if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
-    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    flm::rt::DeviceScope dev_scope_;
+    FLM_HIPC(ctx, dev_scope_.set(flm::rt::device_of(ctx)));
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream, as every *_dev call
     FLM_NCCL(ctx, rccl()->ReduceScatter(d_send, d_recv, recv_words, ncclUint32, ncclSum, cs->comm, s));
     return 0;
@@ -237,7 +239,8 @@ int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t se
     CommState *cs = comm_of(ctx);
     if (!cs) return fail_ctx(ctx, FLM_EINVAL, "no communicator: call flm_comm_init_rank first");
     if (!d_send || !d_recv) return fail_ctx(ctx, FLM_EINVAL, "NULL buffer");
-    FLM_HIPC(ctx, hipSetDevice(flm::rt::device_of(ctx)));
+    flm::rt::DeviceScope dev_scope_;
+    FLM_HIPC(ctx, dev_scope_.set(flm::rt::device_of(ctx)));
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_NCCL(ctx, rccl()->AllGather(d_send, d_recv, send_bytes, ncclUint8, cs->comm, s));
     return 0;
@@ -352,6 +355,7 @@ int wait_previous_exchange(flm_group *g, int r) {
 extern "C" {
 
 int flm_group_init(flm_group **out, int n, const int *devices) {
+    flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!out) return gfail(nullptr, FLM_EINVAL, "flm_group_init: out is NULL");
     *out = nullptr;
     if (n < 1 || n > flm::kMaxParts) return gfail(nullptr, FLM_EINVAL, "flm_group_init: n must be in [1, 16]");
@@ -410,6 +414,7 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
 }
 
 void flm_group_free(flm_group *g) {
+    flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!g) return;
     for (int r = 0; r < (int)g->ctx.size(); ++r) {
         (void)hipSetDevice(g->dev[r]);
@@ -435,6 +440,7 @@ flm_ctx *flm_group_ctx(flm_group *g, int rank) {
 }
 
 int flm_group_sync(flm_group *g) {
+    flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!g) return FLM_EINVAL;
     for (int r = 0; r < g->n; ++r) {
         (void)hipSetDevice(g->dev[r]);
@@ -449,6 +455,7 @@ int flm_group_sync(flm_group *g) {
 // clients and enqueues its fused round; then one reduce-scatter; then each shard comes back.
 int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N, const uint8_t *seeds,
                                const int8_t *signs, int K, size_t L, uint32_t *out) {
+    flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!g) return gfail(nullptr, FLM_EINVAL, "group is NULL");
     if (N < 0 || K < 0) return gfail(g, FLM_EINVAL, "negative N or K");
     if (L == 0) return 0;
@@ -506,6 +513,7 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
 int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, size_t row_pitch, const int *n_rows,
                                    const uint8_t *const *d_seeds, const int8_t *const *d_signs, int K, size_t L,
                                    uint32_t *const *d_shards) {
+    flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!g) return gfail(nullptr, FLM_EINVAL, "group is NULL");
     if (!n_rows || !d_shards || (K > 0 && (!d_seeds || !d_signs))) return gfail(g, FLM_EINVAL, "NULL argument");
     if (L == 0) return 0;

@@ -131,6 +131,29 @@ int set_error(flm_ctx *ctx, int code, const char *msg);
 int device_of(const flm_ctx *ctx);
 hipStream_t stream_of(const flm_ctx *ctx);
 void **comm_slot(flm_ctx *ctx);
+// The calling thread's current device belongs to the caller: every entry point that selects a
+// device (its context's, or each rank's of a group or store) gives the caller's back on return.
+// torch and the agents' own HIP code allocate on the current device, and a group call that left
+// it on its last rank's GPU would move them there.  set() switches only when needed (hipGetDevice
+// is a thread-local read), so a call on the caller's own device costs no hipSetDevice at all.
+struct DeviceScope {
+    int old = -1;
+    DeviceScope() {
+        if (hipGetDevice(&old) != hipSuccess) old = -1;
+    }
+    explicit DeviceScope(int want) : DeviceScope() { (void)set(want); }
+    hipError_t set(int want) {
+        int now = -1;
+        if (hipGetDevice(&now) == hipSuccess && now == want) return hipSuccess;
+        return hipSetDevice(want);
+    }
+    ~DeviceScope() {
+        int now = -1;
+        if (old >= 0 && hipGetDevice(&now) == hipSuccess && now != old) (void)hipSetDevice(old);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+};
 // Upload host rows and seeds and enqueue the fused round over mask window [mask_lo, mask_hi) into
 // d_out (L words) on the context's stream; returns without synchronising.
 int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,

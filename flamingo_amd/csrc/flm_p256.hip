@@ -289,6 +289,12 @@ __device__ __forceinline__ Fe from_mont(const Fe &a) {
     return fe_mul(a, one);
 }
 
+// FLM_INV_BINGCD (default 1): ec_finish inverts by binary GCD (fe_inv_bingcd below); 0 builds
+// Fermat's a^(p-2) for A/B runs
+#ifndef FLM_INV_BINGCD
+#define FLM_INV_BINGCD 1
+#endif
+#if !FLM_INV_BINGCD
 // a^(p-2): p-2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
 __device__ Fe fe_inv(const Fe &a) {
     // x_k = a^(2^k - 1)
@@ -328,6 +334,7 @@ __device__ Fe fe_inv(const Fe &a) {
     r = fe_mul(r, a);                       // 1
     return r;
 }
+#endif  // !FLM_INV_BINGCD
 
 // ---- inversion by binary GCD (ec_finish_kernel's one-lane chain)
 // Pornin, "Optimized Binary GCD for Modular Inversion" (eprint 2020/972), Algorithm 2, with
@@ -339,10 +346,7 @@ __device__ Fe fe_inv(const Fe &a) {
 // matrix to the 256-bit a, b and to the Bezout coefficients u, v mod p (with a Montgomery
 // division by 2^30; -p^-1 = 1 mod 2^30, so the quotient digit is the low 30 bits).  No
 // data-dependent branches, so a wave's lanes never diverge.  ~25k VALU instructions against
-// Fermat's ~73k (266 squarings, 11 multiplications).  FLM_INV_BINGCD=0 builds Fermat for A/B.
-#ifndef FLM_INV_BINGCD
-#define FLM_INV_BINGCD 1
-#endif
+// Fermat's ~73k (266 squarings, 11 multiplications).
 __device__ constexpr uint32_t kR3[8] = {0x0000000au, 0xfffffffdu, 0xfffffff7u, 0xffffffedu,
                                         0xfffffffcu, 0x00000005u, 0x00000001u, 0x00000018u};  // R^3 mod p
 
@@ -1369,10 +1373,16 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
 // write the affine wire point and optionally SHA-256(x||y).
 // flags bit 0: base off-curve, bit 1: an input share was off-curve (ec_mul), bit 2: result at infinity.
-// kFinishLanes lanes per element split the T terms (lane q adds j = q, q + 4, ...), then two
-// LDS tree levels add the four partials: 5 + 2 sequential additions at T = 20 instead of 20.
+// kFinishLanes lanes per element split the T terms (lane q adds j = q, q + kFinishLanes, ...), then
+// log2(kFinishLanes) LDS tree levels add the partials.  At T = 20: 8 lanes make it 3 + 3 sequential
+// additions (lane 0 adds c1 first), 4 lanes 5 + 2 (round 3: 8, FLM_FINISH_LANES for A/B runs).
 // Lane 0 of each element then inverts Z and hashes (the inversion is one lane's chain either way).
-constexpr int kFinishLanes = 4;
+#ifndef FLM_FINISH_LANES
+#define FLM_FINISH_LANES 8
+#endif
+constexpr int kFinishLanes = FLM_FINISH_LANES;
+static_assert(kFinishLanes >= 1 && (kFinishLanes & (kFinishLanes - 1)) == 0 && kFinishLanes <= 64,
+              "kFinishLanes: a power of two dividing the workgroup");
 __global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__restrict__ base,
                                                                const uint32_t *__restrict__ jac, int T, int D,
                                                                int negate, uint8_t *__restrict__ points_out,

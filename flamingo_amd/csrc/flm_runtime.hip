@@ -148,6 +148,11 @@ int fail(flm_ctx *ctx, int code, const char *fmt, ...) {
     return code;
 }
 
+// Select the context's device for the rest of this entry point; the caller's comes back on return.
+#define FLM_ON_DEVICE(ctx)                 \
+    flm::rt::DeviceScope dev_scope_;       \
+    FLM_HIP((ctx), dev_scope_.set((ctx)->device))
+
 #define FLM_HIP(ctx, expr)                                                                            \
     do {                                                                                              \
         hipError_t e_ = (expr);                                                                       \
@@ -864,7 +869,7 @@ int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uin
     if ((N > 0 && !rows) || (K > 0 && (!seeds || !signs)) || !d_out) return fail(ctx, FLM_EINVAL, "NULL argument");
     if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
     if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
@@ -893,7 +898,8 @@ int flm_init(flm_ctx **out, int device) {
     if (e != hipSuccess || n == 0)
         return fail(nullptr, FLM_EHIP, "flm_init: no HIP device visible (%s)", hipGetErrorString(e));
     if (device < 0 || device >= n) return fail(nullptr, FLM_EINVAL, "flm_init: device %d out of range [0,%d)", device, n);
-    e = hipSetDevice(device);
+    flm::rt::DeviceScope dev_scope_;
+    e = dev_scope_.set(device);
     if (e != hipSuccess) return fail(nullptr, FLM_EHIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
     flm_ctx *ctx = new flm_ctx();
     ctx->device = device;
@@ -909,7 +915,7 @@ int flm_init(flm_ctx **out, int device) {
 
 void flm_free(flm_ctx *ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    flm::rt::DeviceScope dev_scope_(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     flm::comm_release(ctx);
     for (StageSlot *s : ctx->slots) (void)hipEventSynchronize(s->done);  // launches on other streams
@@ -953,7 +959,7 @@ int flm_aggregate_unmask(flm_ctx *ctx, const uint32_t *const *rows, int N, const
     if (!out || (N > 0 && !rows) || (K > 0 && (!seeds || !signs))) return fail(ctx, FLM_EINVAL, "NULL argument");
     if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
     if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
@@ -988,7 +994,7 @@ int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     if (K < 0) return fail(ctx, FLM_EINVAL, "negative K");
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     return run_seed_schedule(ctx, d_seeds, d_signs, K, s, nullptr, 0, /*publish=*/true);
 }
 
@@ -999,7 +1005,7 @@ int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, in
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
     if (K != ctx->table_k) return fail(ctx, FLM_EINVAL, "K=%d does not match the seed table (%d)", K, ctx->table_k);
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     int rc = 0;
     Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, s, &rc);
     if (!plan) return rc;
@@ -1014,7 +1020,7 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     int rc = 0;
     if (const int B = small_round_width(ctx, N, K, L, mask_lo, mask_hi)) {
         // one submission; the device seed table is not built, so flm_aggregate_dev must not reuse it
@@ -1064,7 +1070,7 @@ int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitc
     if (L == 0) return fail(ctx, FLM_EINVAL, "L must be > 0");
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     auto *g = new flm_round_graph();
     hipStream_t cs = nullptr;
     bool capturing = false;
@@ -1123,7 +1129,7 @@ int flm_round_graph_launch(flm_ctx *ctx, void *graph, void *stream) {
 int flm_round_graph_destroy(flm_ctx *ctx, void *graph) {
     if (!ctx || !graph) return fail(ctx, FLM_EINVAL, "NULL argument");
     auto *g = static_cast<flm_round_graph *>(graph);
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     g->destroy();
     delete g;
     return 0;
@@ -1143,7 +1149,7 @@ int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, 
     if (K > 0x7fffffff) return fail(ctx, FLM_EINVAL, "too many seeds");
     if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     uint32_t *d_x = nullptr;
     if (x) {
@@ -1180,7 +1186,7 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
     if (!signs_ok(signs, (int)K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, L)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     // small batches (c2: 128 clients x ~15 seeds x 16384 slots): one launch of the small-round
     // kernel, one workgroup per (client, 256-slot tile), instead of a seed schedule + one 1024-thread
     // workgroup per client row.  seg and signs travel in ONE host-to-device copy.
@@ -1214,7 +1220,7 @@ int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t
     if (!seeds || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
     if (slot0 % 16) return fail(ctx, FLM_EINVAL, "slot0 must be a multiple of 16");
     if (int rc = check_range(ctx, slot0 + L)) return rc;
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     FLM_HIP(ctx, ctx->seeds.reserve((size_t)K * 32));
     FLM_HIP(ctx, hipMemcpyAsync(ctx->seeds.p, seeds, (size_t)K * 32, hipMemcpyHostToDevice, ctx->stream));
@@ -1237,7 +1243,7 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     if ((uintptr_t)d_out & 15) return fail(ctx, FLM_EINVAL, "out must be 16-byte aligned");
     if (int rc = check_range(ctx, slot0 + L)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     // +1 signs are written into the staging slot with the work items: no host wait
     return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, d_seeds, K, 0u, L, slot0, d_out, s);
 }
@@ -1251,7 +1257,7 @@ int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs,
     if (slot0 % 16) return fail(ctx, FLM_EINVAL, "slot0 must be a multiple of 16");
     if (!signs_ok(signs, K, nullptr)) return fail(ctx, FLM_EINVAL, "signs must be +1 or -1");
     if (int rc = check_range(ctx, slot0 + L)) return rc;
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     FLM_HIP(ctx, ctx->rows.reserve(pitch * sizeof(uint32_t)));
     FLM_HIP(ctx, hipMemcpyAsync(ctx->rows.p, acc, L * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -1271,7 +1277,7 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (n == 0) return 0;
     if (!key || !nonce || !in || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     uint32_t k[8], nn[2];
     for (int i = 0; i < 8; ++i)
         k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
@@ -1394,7 +1400,7 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     if (D == 0) return 0;
     if ((T > 0 && (!d_shares || !d_lambdas)) || !d_flags) return fail(ctx, FLM_EINVAL, "NULL argument");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
     const int terms = ec_coop(ctx, (size_t)T * D) ? 1 : ctx->tune_ec_terms;
@@ -1413,7 +1419,7 @@ int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const
     if (int rc = ec_dims(ctx, T, D)) return rc;
     if (D == 0) return 0;
     if (T > 0 && (!shares || !lambdas)) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     const size_t nsh = (size_t)T * D * 64;
     FLM_HIP(ctx, ctx->ec_in.reserve(nsh));
     FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)T * 32));
@@ -1450,7 +1456,7 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
     if (int rc = ec_dims(ctx, T, M)) return rc;
     if (M == 0) return 0;
     if (!d_seeds_out || (T > 0 && (!d_shares || !d_lambdas))) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     hipStream_t s = static_cast<hipStream_t>(stream);
     FLM_HIP(ctx, flm::launch_shamir_combine(d_shares, d_lambdas, T, M, d_seeds_out, s));
     return 0;
@@ -1468,7 +1474,7 @@ int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
         return fail(ctx, FLM_EINVAL, "partial rows and dst must be 16-byte aligned");
     if (L > ((uint64_t)1 << 36)) return fail(ctx, FLM_EINVAL, "L=%zu beyond the 2^32-block ChaCha counter", L);
     if (flm::pair_units_count(K, L, nullptr) == 0xFFFFFFFFu) return fail(ctx, FLM_EINVAL, "too many units");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (final_pass) FLM_HIP(ctx, flm::launch_add2(d_p0, d_p1, d_dst, L, s));
     if (L == 0 || K == 0) return 0;
@@ -1480,7 +1486,7 @@ int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
 int flm_flag_set_dev(flm_ctx *ctx, uint32_t *d_ws, void *stream) {
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (!d_ws) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     FLM_HIP(ctx, flm::launch_flag_set(d_ws, static_cast<hipStream_t>(stream)));
     return 0;
 }
@@ -1491,7 +1497,7 @@ int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambd
     if (int rc = ec_dims(ctx, T, M)) return rc;
     if (M == 0) return 0;
     if (!seeds_out || (T > 0 && (!shares || !lambdas))) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     hipStream_t s = ctx->stream;
     FLM_HIP(ctx, ctx->ec_in.reserve((size_t)std::max(T, 1) * M * 32));
     FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)std::max(T, 1) * 32));
@@ -1512,7 +1518,7 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     if (int rc = ec_dims(ctx, 1, n)) return rc;
     if (n == 0) return 0;
     if (!points || !scalars || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     FLM_HIP(ctx, ctx->ec_in.reserve((size_t)n * 64));
     FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)n * 32));
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)n * 96));
@@ -1566,7 +1572,7 @@ int flm_stream_create_cu_mask(flm_ctx *ctx, const uint32_t *mask, int n_words, v
                 ++set;
             }
     if (set == 0) return fail(ctx, FLM_EINVAL, "CU mask selects no CU");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     hipStream_t s = nullptr;
     FLM_HIP(ctx, hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, mask));
     *stream_out = s;
@@ -1575,7 +1581,7 @@ int flm_stream_create_cu_mask(flm_ctx *ctx, const uint32_t *mask, int n_words, v
 
 int flm_stream_destroy(flm_ctx *ctx, void *stream) {
     if (!ctx || !stream) return fail(ctx, FLM_EINVAL, "NULL argument");
-    FLM_HIP(ctx, hipSetDevice(ctx->device));
+    FLM_ON_DEVICE(ctx);
     FLM_HIP(ctx, hipStreamDestroy(static_cast<hipStream_t>(stream)));
     return 0;
 }

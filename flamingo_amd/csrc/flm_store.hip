@@ -131,6 +131,7 @@ void release(flm_store *st) {
 extern "C" {
 
 int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int capacity) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!out) return sfail(nullptr, FLM_EINVAL, "flm_store_create: out is NULL");
     *out = nullptr;
     if ((ctx == nullptr) == (g == nullptr)) return sfail(nullptr, FLM_EINVAL, "flm_store_create: give a context or a group");
@@ -184,6 +185,7 @@ int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int 
 }
 
 void flm_store_free(flm_store *st) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st) return;
     release(st);
     delete st;
@@ -194,6 +196,7 @@ const char *flm_store_last_error(const flm_store *st) { return st ? st->err.c_st
 int flm_store_count(const flm_store *st) { return st ? (int)st->slot.size() : 0; }
 
 int flm_store_add(flm_store *st, int64_t sender, const uint32_t *row, size_t n) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st) return sfail(nullptr, FLM_EINVAL, "store is NULL");
     if (!row || n != st->L) {  // report_process raises on it (:348-349): remembered for flm_store_partial
         ++st->bad;
@@ -225,6 +228,7 @@ int flm_store_add(flm_store *st, int64_t sender, const uint32_t *row, size_t n) 
 }
 
 int flm_store_partial(flm_store *st) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st) return sfail(nullptr, FLM_EINVAL, "store is NULL");
     if (st->bad) return sfail(st, FLM_EINVAL, "Client sends vector of incorrect length.");
     const int G = (int)st->rk.size();
@@ -273,6 +277,7 @@ int flm_store_partial(flm_store *st) {
 }
 
 int flm_store_partial_wait(flm_store *st, float *gpu_ms) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st) return sfail(nullptr, FLM_EINVAL, "store is NULL");
     if (!st->have_partial) return sfail(st, FLM_EINVAL, "no partial sum enqueued");
     FLM_SHIP(st, hipSetDevice(st->rk[0].device));
@@ -282,6 +287,7 @@ int flm_store_partial_wait(flm_store *st, float *gpu_ms) {
 }
 
 int flm_store_partial_host(flm_store *st, uint32_t *out) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st || !out) return sfail(st, FLM_EINVAL, "NULL argument");
     if (!st->have_partial) return sfail(st, FLM_EINVAL, "no partial sum enqueued");
     for (StoreRank &k : st->rk) {
@@ -298,6 +304,7 @@ int flm_store_partial_host(flm_store *st, uint32_t *out) {
 }
 
 int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *out) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st || !out || K < 0 || (K > 0 && (!seeds || !signs))) return sfail(st, FLM_EINVAL, "bad argument");
     if (!st->have_partial) return sfail(st, FLM_EINVAL, "no partial sum: call flm_store_partial at report");
     for (int k = 0; k < K; ++k)
@@ -335,6 +342,7 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
 }
 
 int flm_store_reset(flm_store *st) {
+    flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st) return sfail(nullptr, FLM_EINVAL, "store is NULL");
     st->slot.clear();
     st->bad = 0;
