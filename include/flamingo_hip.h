@@ -32,6 +32,9 @@
  *  - One context per host thread; a context binds one GPU (one process per
  *    GPU).  Create it lazily, after any fork (SA_ServiceAgent.py:562 forks a
  *    multiprocessing.Pool).
+ *  - Every entry point leaves the calling thread's current HIP device as it
+ *    found it: a call selects its context's device (or each rank's, for a
+ *    group or store) only for its own duration.
  */
 #ifndef FLAMINGO_HIP_H
 #define FLAMINGO_HIP_H
