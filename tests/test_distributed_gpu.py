@@ -1,4 +1,4 @@
-"""The pipelined multi-GPU round's RCCL path on a one-GPU box: tools/probes/rccl_async_smoke.py runs
+"""The pipelined multi-GPU round's RCCL path on a one-GPU box: tools/rccl_async_smoke.py runs
 ShardedRound(buffers=2) with its async reduce-scatter forced on a one-rank nccl (RCCL) group and
 checks every round against the synchronous round (the driver's 8-GPU run uses the same code)."""
 import os

@@ -9,7 +9,7 @@ import sys
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flamingo_amd import MaskEngine  # noqa: E402
 from flamingo_amd.distributed import ShardedRound, init_rccl  # noqa: E402
 
