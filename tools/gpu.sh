@@ -12,7 +12,7 @@
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
-#   py:SCRIPT    python tools/SCRIPT (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
+#   py:SCRIPT[:ARG]  python tools/SCRIPT [ARG] (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
 TAG=${1:?usage: tools/gpu.sh TAG STEP...}
 shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -54,8 +54,10 @@ for step in "$@"; do
       bash tools/gpu_clock.sh "$TAG" > "$O/${TAG}_clock_run.log" 2>&1 || exit 1 ;;
     py:*)
       s=${step#py:}
+      a=""
+      case $s in *:*) a=${s#*:}; s=${s%%:*} ;; esac   # py:SCRIPT:ARG passes one argument
       n=$(basename "${s%.py}")
-      timeout -k 10 600 python -u "tools/$s" > "$O/${TAG}_$n.log" 2>&1 || { tail -20 "$O/${TAG}_$n.log"; exit 1; }
+      timeout -k 10 600 python -u "tools/$s" $a > "$O/${TAG}_$n.log" 2>&1 || { tail -20 "$O/${TAG}_$n.log"; exit 1; }
       tail -5 "$O/${TAG}_$n.log" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
