@@ -7,8 +7,10 @@
 // and the clients/committee do single scalar multiplications (ECDH :256-263,
 // ElGamal :434-447, decryption shares :397-400).  All of it is 256-bit modular
 // arithmetic on independent points -- one lane per (term, pair) scalar
-// multiplication, one lane per pair for the combine -- so this is plain VALU
-// integer work: no MFMA, no LDS.
+// multiplication (or four cooperating waves per 64 of them, exchanging field
+// elements through LDS), a few lanes per pair for the combine -- so this is
+// VALU integer work: no MFMA.  A small batch is one latency chain, bound by the
+// quarter-rate v_mad_u64_u32 on its critical path.
 //
 // Field: p = 2^256 - 2^224 + 2^192 + 2^96 - 1, eight 32-bit limbs little
 // endian, Montgomery form with R = 2^256 (-p^-1 mod 2^32 = 1, so the CIOS
