@@ -389,6 +389,14 @@ def main():
                                    M=int(round(c5["online_mean"])), T=20)
             rec["server_reconstruction_ms"] = round(rec["gpu_ms"] + c5["ms_per_round"], 4)
             c5["seed_recovery"] = rec
+            # one rank's share on 8 GPUs (dist_recon: every rank recovers all m_i and ceil(D/8) pairs):
+            # the EC chain that sets the 8-GPU latency from the shares, measured on this one GPU
+            d8 = -(-int(round(c5["dropout_pairs_D_mean"])) // 8)
+            r8 = measure_recovery(eng, torch, D=d8, M=int(round(c5["online_mean"])), T=20)
+            c5["seed_recovery_one_rank_of_8"] = {
+                "what": "the seed recovery one rank of an 8-GPU c5 runs (all m_i, ceil(D/8) dropout pairs), "
+                        "timed alone on this GPU: the latency floor of shares -> final_sum at G = 8",
+                "D_pairs": d8, "online_M": r8["online_M"], "gpu_ms": r8["gpu_ms"], "correct": r8["correct"]}
         if not args.no_copy:
             res["with_copy"] = with_copy(eng, torch, rows_on, sseeds, ssigns, L, len(online))
         if not args.no_cpu:
