@@ -306,6 +306,7 @@ def main():
     if G > 1:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     ok = bool(okt.item())
+    xch = time_exchange(torch, dist, rnd, stream, coll_dev, L) if G > 1 else None
 
     ms_per_step = elapsed / args.steps * 1e3
     bytes_round = 4.0 * len(online) * L + 4.0 * L
@@ -325,7 +326,8 @@ def main():
                  "collective": (("library RCCL communicator (ncclReduceScatter, ncclUint32)" if rnd.comm == "rccl"
                                  else f"torch.distributed {args.dist_backend} reduce_scatter_tensor")
                                 if G > 1 else None),
-                 "rccl_comm_ranks": eng.comm_size()[0] if rnd.comm == "rccl" else None},
+                 "rccl_comm_ranks": eng.comm_size()[0] if rnd.comm == "rccl" else None,
+                 "reduce_scatter": xch},
         "clock_settle": settle,
         "data": "synthetic: valid masked rows y_i = 1 + PRG(m_i) +- PRG(s_ij) made on-GPU from SHA-256 bench "
                 "seeds, neighbour graph of util/param.py findNeighbors (root 0^32, iter 1, o=1)",
@@ -638,6 +640,32 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
                              "ms": round(float(np.mean(cm_ms)), 4), "mask_words": int(np.mean(cm_words)),
                              "G_words/s": round(float(np.mean(cm_words)) / float(np.mean(cm_ms)) / 1e6, 1)},
             **extra}
+
+
+def time_exchange(torch, dist, rnd, stream, coll_dev, L, reps=10):
+    """The round's one collective on its own: `reps` reduce-scatters of the partial (Lp words, the
+    same call ShardedRound makes) bracketed by HIP events on the round's stream after a barrier,
+    max over ranks.  Outside the timed loop; there the collective overlaps the next round's kernel."""
+    torch.cuda.synchronize()
+    dist.barrier()
+    rnd.exchange(stream)                                  # warm
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        rnd.exchange(stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    t = torch.tensor([ms], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item())
+    nbytes = 4 * rnd.Lp
+    return {"what": "one reduce-scatter of the Lp-word partial, HIP events on the round's stream, max over ranks "
+                    "(in the timed loop it overlaps the next round's kernel)",
+            "ms": round(ms, 4), "bytes_per_rank": nbytes,
+            "bus_GB_per_s": round(nbytes * (rnd.world - 1) / rnd.world / (ms * 1e-3) / 1e9, 1)}
 
 
 def measure_recovery(eng, torch, D, M, T, steps=10):
