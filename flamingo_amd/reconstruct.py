@@ -52,12 +52,14 @@ import torch
 
 class ServerReconstruction:
     def __init__(self, engine, device=None, pass1_min_items: int = 1024, ec_cus: int = 0, cu_pick: str = "stride",
-                 pair_split: float = 0.0, pair_queue: bool = False, ec_terms: int = 1, ec_spread: int = 0):
+                 pair_split: float = 0.0, pair_queue: bool = False, ec_terms: int = 1, ec_spread: int = 0,
+                 ec_coop: int = 0):
         self.eng = engine
         if ec_terms not in (1, 2, 4):
             raise ValueError("ec_terms must be 1, 2 or 4")
         self.ec_terms = int(ec_terms)
         self.ec_spread = int(ec_spread)   # KiB of LDS per EC workgroup on the confined CUs (flm_set_tuning ec_spread)
+        self.ec_coop = int(ec_coop)       # on the confined CUs: 0 one lane per product, 1 four cooperating waves
         self.pass1_min_items = pass1_min_items
         if not 0.0 <= pair_split < 1.0:
             raise ValueError("pair_split must be in [0, 1)")
@@ -110,11 +112,13 @@ class ServerReconstruction:
     def _ec_combine(self, c1, pair_shares, lambdas, p_seeds, flags):
         """The threshold-ElGamal combine on the side stream.  Confined to ec_cus CUs it fills them,
         so the one-lane-per-product kernel (fewer instructions) beats the cooperative one there
-        (profiles/r02_recon_coop.log), and `ec_terms` products per lane share one chain of
+        (profiles/r02_recon_coop.log; re-checked after round 3's shorter chain, ec_coop=1 on 24-48
+        first CUs: 6.71-8.72 ms against 6.63-7.70 for two Straus terms per lane,
+        profiles/r03_recon_coop_confined_sweep.log), and `ec_terms` products per lane share one chain of
         doublings (Straus: 2 terms on 24 CUs 8.05 ms vs 1 term on 32 CUs 8.46, profiles/r02_straus_recon.log);
         unconfined, the library's auto choice stands."""
         if self.ec_cus > 0:
-            self.eng.set_tuning("ec_coop", 0)
+            self.eng.set_tuning("ec_coop", self.ec_coop)
             self.eng.set_tuning("ec_terms", self.ec_terms)
             self.eng.set_tuning("ec_spread", self.ec_spread)
         try:

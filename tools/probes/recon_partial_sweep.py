@@ -39,6 +39,9 @@ for cus in (16, 24, 32, 40):
     for pick in ("first", "stride"):
         for terms in (1, 2):
             cases.append(dict(ec_cus=cus, cu_pick=pick, pair_queue=True, ec_terms=terms, pass1_min_items=4096))
+if "--coop" in sys.argv:   # round 3: the cooperative kernel on the confined EC CUs against the per-lane Straus default
+    cases = [dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=t, ec_coop=k, pass1_min_items=4096)
+             for c in (24, 32, 40, 48) for (t, k) in ((2, 0), (1, 1))] * 2
 for kw in cases:
     rec = ServerReconstruction(eng, **kw)
     args = (S, L, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], out)
