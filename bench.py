@@ -425,6 +425,9 @@ RECON_QUEUE_MIN_ITEMS = 4096  # its pass 1 plan: 4 same-tile row/seed parts per 
                              # 8.17 ms vs 8.28 at 1024 items (profiles/r02_recon_minitems.log)
 RECON_QUEUE_EC_FRAC = 24 / 256  # EC CUs of the pair-queue schedule, with RECON_QUEUE_EC_TERMS combine terms per lane
 RECON_QUEUE_EC_TERMS = 2        # (Straus): 16 / 24 / 32 CUs -> 9.78 / 8.05 / 8.28 ms; one term per lane on 32 CUs
+RANK_EC_FRAC = 72 / 256  # EC CUs of one rank's CU-partitioned sharded reconstruction at G >= 4: one G = 8 rank's
+                         # shares -> final 1.39-1.40 ms on 72 or 96 CUs against 1.63 unpartitioned (64 / 80 CUs
+                         # bimodal; tools/probes/rank8_overlap_probe.py, profiles/r03_rank8_overlap_*.log)
 RECON_STRIDE_EC_FRAC = 32 / 256  # the same queue schedule with the EC CUs strided over the logical ids: alone, the
                                  # combine runs 3.84 ms on 24 strided CUs against 5.36 on the first 24
                                  # (profiles/r02_ec_pick.log); beside the unmask 32 strided CUs measured best
@@ -930,9 +933,14 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
     m = np.frombuffer(b"".join(P.bench_seed("c5", i) for i in range(N)), np.uint8).reshape(N, 32)
     stream = torch.cuda.current_stream()
     rec = ShardedReconstruction(eng, L, comm=comm or ("rccl" if backend == "nccl" else "torch"))
+    # from G = 4 on, one rank's pair chunk is a few dozen cooperative workgroups: also time the
+    # schedule with the combine on its own CUs (dist_recon ec_cus; RANK_EC_FRAC of the CUs)
+    rec_cu = None
+    if G >= 4 and eng.cu_count() >= 64:
+        rec_cu = ShardedReconstruction(eng, L, comm=rec.comm, ec_cus=int(round(RANK_EC_FRAC * eng.cu_count() / 8)) * 8)
     out = torch.empty(rec.S, dtype=torch.int32, device=dev)
     per_round, oks, Ds = [], True, []
-    rep_ms, fp_ms = [], []
+    rep_ms, fp_ms, fp_cu_ms = [], [], []
     S_shard = torch.empty(rec.S, dtype=torch.int32, device=dev)
     cache = {}
     coll = dev if backend == "nccl" else torch.device("cpu")
@@ -990,6 +998,10 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
         out.fill_(0)
         fp_ms.append(timed(lambda: rec.run_from_partial(S_shard, *args[1:], stream=stream)))
         oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
+        if rec_cu is not None:
+            out.fill_(0)
+            fp_cu_ms.append(timed(lambda: rec_cu.run_from_partial(S_shard, *args[1:], stream=stream)))
+            oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
         Ds.append(D)
         del rows
     okt = torch.tensor([1 if oks else 0], device=coll)
@@ -1003,7 +1015,12 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
                                     "shares_to_final_ms": round(float(np.mean(fp_ms)), 4),
                                     "what": "ShardedReconstruction.report (rows -> reduce-scattered S shards, at "
                                             "report time) and run_from_partial (shares -> final over each rank's "
-                                            "S shard: the all-gather of pair keys is the one exchange)"},
+                                            "S shard: the all-gather of pair keys is the one exchange)",
+                                    **({"shares_to_final_ec_cus_ms": round(float(np.mean(fp_cu_ms)), 4),
+                                        "ec_cus": rec_cu.ec_cus,
+                                        "what_ec_cus": "the same with the combine on its own first ec_cus CUs and "
+                                                       "Shamir + self masks on the rest (dist_recon ec_cus)"}
+                                       if rec_cu is not None else {})},
             "correct": bool(okt.item()),
             "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
                         "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "

@@ -871,6 +871,9 @@ constexpr int kCoopSlots = 11;
 #ifndef FLM_COOP_MODJ
 #define FLM_COOP_MODJ 1
 #endif
+#ifndef FLM_COOP_PRIO
+#define FLM_COOP_PRIO 1  // s_setprio(3) in ec_mul_coop_kernel (0: A/B builds)
+#endif
 
 // lane-major slots: a lane's 8 words are 32 contiguous bytes, moved with two 16-byte LDS ops
 // (0.5-1 % faster than word-major single-dword ops, profiles/r02_ab_coop_b128.log)
@@ -1252,6 +1255,11 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
                                                                    int per_element, int T, int D,
                                                                    uint32_t *__restrict__ jac,
                                                                    uint32_t *__restrict__ flags) {
+#if FLM_COOP_PRIO
+    // latency-bound like ec_mul_kernel: beside the unmask on another stream (the unpartitioned
+    // overlap, every rank of a sharded reconstruction) these waves issue first
+    __builtin_amdgcn_s_setprio(3);
+#endif
     __shared__ __attribute__((aligned(16))) uint32_t S[kCoopSlots * 8 * 64];  // exchange slots, 512 words each
     __shared__ __attribute__((aligned(16))) uint32_t tab[9 * 24 * 64];  // (2t+1) P, t = 0..7, + a spare row
     const int lane = threadIdx.x & 63;

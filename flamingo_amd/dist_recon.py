@@ -47,7 +47,16 @@ def pair_chunk(D: int, world: int, rank: int):
 
 
 class ShardedReconstruction:
-    def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None):
+    """ec_cus > 0 partitions the rank's CUs (flm_stream_create_cu_mask): the combine runs on the first
+    `ec_cus` CUs (cu_pick), Shamir and the self-mask pass on the rest, and the caller's stream joins
+    both before the all-gather.  One rank's share of the pairs is a few dozen cooperative workgroups,
+    so on its own CUs the chain keeps its lone-wave speed instead of sharing SIMDs with the pass:
+    one rank of G = 8 at c5 from its S shard 1.63 ms unpartitioned against 1.39-1.40 ms on 72 or 96
+    EC CUs (tools/probes/rank8_overlap_probe.py, profiles/r03_rank8_overlap_*.log; 64 and 80 CUs
+    came out bimodal there).  Default 0: unpartitioned."""
+
+    def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None, ec_cus: int = 0,
+                 cu_pick: str = "first"):
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -60,7 +69,18 @@ class ShardedReconstruction:
         if comm is None:
             comm = "rccl" if (self.world > 1 and engine.comm_size() == (self.world, self.rank)) else "torch"
         self.comm = comm
-        self.side = torch.cuda.Stream(device=self.device)
+        self.ec_cus = int(ec_cus)
+        self.pass_stream = None
+        if self.ec_cus > 0:
+            from .reconstruct import pick_cus
+            n = engine.cu_count()
+            if not 0 < self.ec_cus < n:
+                raise ValueError(f"ec_cus={ec_cus} must be in (0, {n})")
+            ec = pick_cus(n, self.ec_cus, cu_pick)
+            self.side = engine.cu_stream(ec)
+            self.pass_stream = engine.cu_stream([c for c in range(n) if c not in set(ec)])
+        else:
+            self.side = torch.cuda.Stream(device=self.device)
         self._bufs = {}
 
     def _buf(self, name, shape, dtype, fill=None):
@@ -71,6 +91,20 @@ class ShardedReconstruction:
                 b.fill_(fill)
             self._bufs[name] = b
         return b
+
+    def _pass_begin(self, ready, main):
+        """The stream Shamir and the self-mask pass run on: the caller's, or (ec_cus > 0) the
+        CU-partitioned pass stream, ordered after the caller's work so far."""
+        if self.pass_stream is None:
+            return main
+        self.pass_stream.wait_event(ready)
+        return self.pass_stream
+
+    def _pass_end(self, ps, main):
+        if ps is not main:
+            ev = torch.cuda.Event()
+            ev.record(ps)
+            main.wait_event(ev)
 
     def _all_gather(self, chunk, gathered, stream):
         if self.world == 1:
@@ -127,9 +161,11 @@ class ShardedReconstruction:
             eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
         done = torch.cuda.Event()
         done.record(self.side)
-        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+        ps = self._pass_begin(ready, main)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=ps)
         eng.aggregate_unmask_dev(rows, m_seeds, neg, part[0], L=self.L, mask_lo=self.lo, mask_hi=self.hi,
-                                 stream=main)
+                                 stream=ps)
+        self._pass_end(ps, main)
         if D:
             main.wait_event(done)
             self._all_gather(chunk, gathered, main)
@@ -181,10 +217,12 @@ class ShardedReconstruction:
             eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
         done = torch.cuda.Event()
         done.record(self.side)
-        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=main)
+        ps = self._pass_begin(ready, main)
+        eng.shamir_combine_dev(mi_shares, lambdas, m_seeds, stream=ps)
         src = S_shard[: self.S].view(1, self.S)
         if n > 0:
-            eng.aggregate_unmask_dev(src, m_seeds, neg, part[0] if D else out, L=n, prg_slot0=self.lo, stream=main)
+            eng.aggregate_unmask_dev(src, m_seeds, neg, part[0] if D else out, L=n, prg_slot0=self.lo, stream=ps)
+        self._pass_end(ps, main)
         if D:
             main.wait_event(done)
             self._all_gather(chunk, gathered, main)

@@ -71,6 +71,19 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
     good &= bool(np.all(out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32) == len(on)))
     print(f"rank {r}/{G} N={N} L={L} D={D} from report partial: S shard and out==|U| {good}", flush=True)
     ok &= good
+    # the CU-partitioned schedule: combine on its own CUs, Shamir + self masks on the rest
+    rec_cu = ShardedReconstruction(eng, L, ec_cus=max(8, eng.cu_count() // 4 // 8 * 8))
+    for name, fn in (("run", lambda: rec_cu.run(r_rows, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]),
+                                                t(R["pair_shares"][:, a:b]), t(R["pair_signs"]), D, out)),
+                     ("from report partial", lambda: rec_cu.run_from_partial(
+                         S_shard, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]), t(R["pair_shares"][:, a:b]),
+                         t(R["pair_signs"]), D, out))):
+        out.fill_(7)
+        fn()
+        torch.cuda.synchronize()
+        good = bool(np.all(out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32) == len(on)))
+        print(f"rank {r}/{G} N={N} L={L} D={D} ec_cus={rec_cu.ec_cus} {name}: out==|U| {good}", flush=True)
+        ok &= good
 okt = torch.tensor([1 if ok else 0])
 if backend == "nccl":
     okt = okt.to(dev)
