@@ -425,7 +425,7 @@ RECON_QUEUE_MIN_ITEMS = 4096  # its pass 1 plan: 4 same-tile row/seed parts per 
                              # 8.17 ms vs 8.28 at 1024 items (profiles/r02_recon_minitems.log)
 RECON_QUEUE_EC_FRAC = 24 / 256  # EC CUs of the pair-queue schedule, with RECON_QUEUE_EC_TERMS combine terms per lane
 RECON_QUEUE_EC_TERMS = 2        # (Straus): 16 / 24 / 32 CUs -> 9.78 / 8.05 / 8.28 ms; one term per lane on 32 CUs
-RANK_EC_FRAC = 72 / 256  # EC CUs of one rank's CU-partitioned sharded reconstruction at G >= 4: one G = 8 rank's
+RANK_EC_FRAC = 72 / 256  # EC CUs of one rank's CU-partitioned sharded reconstruction at G >= 8: one G = 8 rank's
                          # shares -> final 1.39-1.40 ms on 72 or 96 CUs against 1.63 unpartitioned (64 / 80 CUs
                          # bimodal; tools/probes/rank8_overlap_probe.py, profiles/r03_rank8_overlap_*.log)
 RECON_STRIDE_EC_FRAC = 32 / 256  # the same queue schedule with the EC CUs strided over the logical ids: alone, the
@@ -933,10 +933,11 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
     m = np.frombuffer(b"".join(P.bench_seed("c5", i) for i in range(N)), np.uint8).reshape(N, 32)
     stream = torch.cuda.current_stream()
     rec = ShardedReconstruction(eng, L, comm=comm or ("rccl" if backend == "nccl" else "torch"))
-    # from G = 4 on, one rank's pair chunk is a few dozen cooperative workgroups: also time the
-    # schedule with the combine on its own CUs (dist_recon ec_cus; RANK_EC_FRAC of the CUs)
+    # at G = 8 one rank's self-mask pass is shorter than its combine's chain: also time the schedule
+    # with the combine on its own CUs (dist_recon ec_cus; RANK_EC_FRAC of the CUs).  At G = 2 / 4 the
+    # pass on the remaining CUs is the longer leg and it loses (profiles/r03_rank_overlap_G{2,4}.log)
     rec_cu = None
-    if G >= 4 and eng.cu_count() >= 64:
+    if G >= 8 and eng.cu_count() >= 64:
         rec_cu = ShardedReconstruction(eng, L, comm=rec.comm, ec_cus=int(round(RANK_EC_FRAC * eng.cu_count() / 8)) * 8)
     out = torch.empty(rec.S, dtype=torch.int32, device=dev)
     per_round, oks, Ds = [], True, []

@@ -53,7 +53,9 @@ class ShardedReconstruction:
     so on its own CUs the chain keeps its lone-wave speed instead of sharing SIMDs with the pass:
     one rank of G = 8 at c5 from its S shard 1.63 ms unpartitioned against 1.39-1.40 ms on 72 or 96
     EC CUs (tools/probes/rank8_overlap_probe.py, profiles/r03_rank8_overlap_*.log; 64 and 80 CUs
-    came out bimodal there).  Default 0: unpartitioned."""
+    came out bimodal there).  At G = 4 / 2 the self-mask pass on the remaining CUs is the longer leg
+    and the partitioned schedule loses (1.75 -> 2.21 ms, 3.01 -> 4.07 ms; r03_rank_overlap_G{4,2}.log).
+    Default 0: unpartitioned."""
 
     def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None, ec_cus: int = 0,
                  cu_pick: str = "first"):

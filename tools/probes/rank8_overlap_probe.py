@@ -16,7 +16,8 @@ from flamingo_amd import MaskEngine  # noqa: E402
 from flamingo_amd.reconstruct import ServerReconstruction  # noqa: E402
 from flamingo_amd.synthetic import recovery_round  # noqa: E402
 
-N, L, G = 4096, 1 << 20, 8
+N, L = 4096, 1 << 20
+G = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--G=")), 8))   # the rank shape of G GPUs
 L8 = L // G
 eng = MaskEngine(0)
 dev = torch.device("cuda:0")
@@ -46,6 +47,10 @@ for cus in (40, 48, 64):
                        dict(ec_cus=cus, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=mi), True))
 if "--coop-only" in sys.argv:
     cases = cases[:2] + cases[4:]
+if "--shapes" in sys.argv:   # the unpartitioned overlap against the partitioned schedule at 72 / 96 / 128 CUs
+    cases = cases[:2] + [(f"cu_split_coop_{c}_items4096",
+                          dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=4096), True)
+                         for c in (72, 96, 128)] * 2
 if "--coop-fine" in sys.argv:   # around the best of --coop-only, two passes
     cases = cases[:2] + [(f"cu_split_coop_{c}_items{mi}",
                            dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=mi), True)
