@@ -111,6 +111,72 @@ def world_check(gpus: int, world: int, backend: str, devices: int) -> str:
     return ""
 
 
+def client_table(torch, P, m, nbrs, c0, c1, dev):
+    """The client seed table of clients [c0, c1) (ids are global: SA_ClientAgent.py:304-324):
+    seg (host), seeds (device), signs (host), for flm_client_mask_dev."""
+    seg_l, seeds_l, signs_l = [0], [], []
+    for i in range(c0, c1):
+        seeds_l.append(m[i].tobytes()); signs_l.append(1)
+        for j in sorted(nbrs[i]):
+            seeds_l.append(P.synthetic_pair_seed(i, j)); signs_l.append(1 if i < j else -1)
+        seg_l.append(len(seeds_l))
+    cseeds = np.frombuffer(b"".join(seeds_l), np.uint8).reshape(-1, 32)
+    return np.array(seg_l, np.int64), torch.from_numpy(cseeds.copy()).to(dev), np.array(signs_l, np.int8)
+
+
+def shard_windows(L, G, n=1024):
+    """The parity windows of a G-way sharded round: the first and the last n slots of every
+    non-empty shard (flm_shard_bounds), as (rank, start, length)."""
+    from flamingo_amd.distributed import shard_bounds
+    wins = []
+    for r in range(G):
+        lo, hi = shard_bounds(L, G, r)
+        if hi <= lo:
+            continue
+        w = min(n, hi - lo)
+        for a in sorted({lo, hi - w}):
+            wins.append((r, a, w))
+    return wins
+
+
+def oracle_windows(torch, dist, rows, out_mine, lo, G, rank, seeds, signs, L, coll_dev, n=1024):
+    """In-run parity of a (possibly sharded) round against the C oracle, outside the timed region:
+    for the first and last n slots of every rank's shard, every rank sums ITS rows over the window
+    on the host (uint64), an all-reduce adds the ranks' partial sums (G > 1), and each rank compares
+    its own shard's windows of `out_mine` (slots lo.. of the round's output) with
+    oracle.aggregate_unmask(S_window, seeds, signs, slot0=a) -- the reference's
+    vec_sum_partial + cancel_vec + mi_vec (SA_ServiceAgent.py:346-350, 529-605) over that window.
+    Results are all-reduced (MIN): True only if every rank's windows match bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # checker only
+    wins = shard_windows(L, G, n)
+    host_rows = [rows[:, a:a + w].cpu().numpy().view(np.uint32) if rows is not None and rows.shape[0]
+                 else np.zeros((0, w), np.uint32) for _, a, w in wins]
+    part = np.concatenate([h.sum(axis=0, dtype=np.uint64) for h in host_rows]).astype(np.int64)
+    coll_dev = torch.device("cpu") if coll_dev is None else coll_dev
+    t = torch.from_numpy(part).to(coll_dev)
+    if G > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    S_all = (t.cpu().numpy() % (1 << 32)).astype(np.uint32)
+    seeds_h = seeds.cpu().numpy() if hasattr(seeds, "cpu") else np.asarray(seeds, np.uint8)
+    signs_h = signs.cpu().numpy() if hasattr(signs, "cpu") else np.asarray(signs, np.int8)
+    ok, o, mine = True, 0, []
+    for r, a, w in wins:
+        if r == rank:
+            want = O.aggregate_unmask(S_all[o:o + w][None], seeds_h, signs_h, L=w, slot0=a, threads=8)
+            got = out_mine[a - lo:a - lo + w].cpu().numpy().view(np.uint32)
+            ok &= bool(np.array_equal(got, want))
+            mine.append([a, w])
+        o += w
+    okt = torch.tensor([1 if ok else 0], device=coll_dev)
+    if G > 1:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    return {"match": bool(okt.item()), "windows": [[a, w] for _, a, w in wins], "seeds_K": int(seeds_h.shape[0]),
+            "what": "oracle/flamingo_oracle.c aggregate_unmask over the first and last slots of every rank's shard "
+                    "(row sums all-reduced over the ranks), bit-exact against the GPU output, outside the timed "
+                    "region"}
+
+
 def group_leg_main(args):
     """`bench.py --group-leg`: the c4 inputs of main() (same seeds, graph and offline set), then
     measure_group; prints one JSON object."""
@@ -212,17 +278,7 @@ def main():
     m = np.frombuffer(b"".join(P.bench_seed(cfg, i) for i in range(N)), np.uint8).reshape(N, 32)
     nbrs = P.neighbor_graph(b"\x00" * 32, 1, N, 1, encrypt=eng.chacha20_encrypt)
     c0, c1 = client_bounds(N, G, rank)
-    # client seed table of my clients (ids are global: SA_ClientAgent.py:304-324)
-    seg_l, seeds_l, signs_l = [0], [], []
-    for i in range(c0, c1):
-        seeds_l.append(m[i].tobytes()); signs_l.append(1)
-        for j in sorted(nbrs[i]):
-            seeds_l.append(P.synthetic_pair_seed(i, j)); signs_l.append(1 if i < j else -1)
-        seg_l.append(len(seeds_l))
-    seg = np.array(seg_l, np.int64)
-    cseeds = np.frombuffer(b"".join(seeds_l), np.uint8).reshape(-1, 32)
-    csigns = np.array(signs_l, np.int8)
-    d_cseeds = torch.from_numpy(cseeds.copy()).to(dev)
+    seg, d_cseeds, csigns = client_table(torch, P, m, nbrs, c0, c1, dev)
 
     g = np.random.Generator(np.random.PCG64(12345))
     n_off = int(round(args.dropout * N))
@@ -307,6 +363,17 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     ok = bool(okt.item())
     xch = time_exchange(torch, dist, rnd, stream, coll_dev, L) if G > 1 else None
+    # every rank's dominant-kernel time: the line shows the imbalance between ranks
+    k_all = [kms]
+    if G > 1:
+        kt = torch.tensor([kms], dtype=torch.float64, device=coll_dev)
+        k_all = [torch.zeros_like(kt) for _ in range(G)]
+        dist.all_gather(k_all, kt)
+        k_all = [float(x.item()) for x in k_all]
+    # in-run parity of the timed round: windows of every rank's shard against the C oracle
+    parity = None
+    if not args.profile:
+        parity = oracle_windows(torch, dist, rows_on, out, rnd.lo, G, rank, d_seeds, d_signs, L, coll_dev)
 
     ms_per_step = elapsed / args.steps * 1e3
     bytes_round = 4.0 * len(online) * L + 4.0 * L
@@ -322,6 +389,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "u32", "correct": ok,
+        "checked_against_oracle": parity,
         "comm": {"world": G, "backend": args.dist_backend if G > 1 else None,
                  "collective": (("library RCCL communicator (ncclReduceScatter, ncclUint32)" if rnd.comm == "rccl"
                                  else f"torch.distributed {args.dist_backend} reduce_scatter_tensor")
@@ -341,6 +409,8 @@ def main():
                      "frac": round(ach_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "items_kernel<1>", "kernel_ms": round(kms, 4),
                      "kernel_ms_p10_p50_p90": [round(float(x), 4) for x in kq],
+                     "kernel_ms_per_rank": {"min": round(min(k_all), 4), "max": round(max(k_all), 4),
+                                            "ranks": [round(x, 4) for x in k_all]},
                      "bytes_per_launch": 4 * rows_rank * L + 4 * L},
         "roofline_valu": {"bound": "valu", "mask_words_per_launch": int(words), "ops_per_word": CHACHA_OPS_PER_WORD,
                           "achieved_tops": round(valu_tops, 2), "peak_tops": round(VALU_PEAK_TOPS, 1),
@@ -372,11 +442,32 @@ def main():
         pk = practical_peak(eng, torch, rows_on, L, stream)
         res["roofline"]["practical_peak"] = pk
         res["roofline"]["frac_of_practical_peak"] = round(ach_gbs / pk["GB/s"], 4)
+    if not args.profile and not args.no_variants:
+        # every rank at once (each over its own rows and its own slot shard), rank 0 reports
+        po = variant_pairs_only(eng, torch, rows_on, nbrs, N, L, stream, P, rnd.lo, rnd.hi)["pairs_only"]
+        po["frac_of_practical_peak"] = round(po["GB/s"] / res["roofline"]["practical_peak"]["GB/s"], 4)
+        if G > 1:
+            vt = torch.tensor([po["kernel_ms"]], dtype=torch.float64, device=coll_dev)
+            v_all = [torch.zeros_like(vt) for _ in range(G)]
+            dist.all_gather(v_all, vt)
+            po["kernel_ms_per_rank"] = [round(float(x.item()), 4) for x in v_all]
+        res["variants"] = {"pairs_only": po}
+    if G > 1 and not args.profile and not args.no_cpu:
+        # the reference's CPU path beside the G-GPU number: rank 0 rebuilds every client's row, runs
+        # the reference loop on the whole c4 workload and compares it with the gathered shards
+        full_out = gather_full_out(torch, dist, out, rnd.S, L, G, coll_dev)
+        if rank == 0:
+            seg_a, d_cs_a, cs_a = client_table(torch, P, m, nbrs, 0, N, dev)
+            rows_all = torch.empty((N, L), dtype=torch.int32, device=dev)
+            eng.client_mask_dev(seg_a, d_cs_a, cs_a, rows_all, L, stream=stream)
+            if len(online) != N:
+                rows_all = rows_all[torch.from_numpy(online).to(dev)].contiguous()
+            res["cpu_baseline"] = cpu_baseline(rows_all, sseeds, ssigns, L, full_out)
+            res["cpu_baseline"]["gpu_side"] = f"the {G} ranks' output shards, gathered"
+            del rows_all, d_cs_a
+            torch.cuda.empty_cache()
+        dist.barrier()
     if rank == 0 and G == 1 and not args.profile:
-        if not args.no_variants:
-            res["variants"] = variant_pairs_only(eng, torch, rows_on, m, nbrs, online, L, stream, P)
-            po = res["variants"]["pairs_only"]
-            po["frac_of_practical_peak"] = round(po["GB/s"] / res["roofline"]["practical_peak"]["GB/s"], 4)
         if not args.no_group:
             res["group"] = group_leg_subprocess(args)
         if not args.no_configs:
@@ -477,7 +568,8 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     stream = torch.cuda.current_stream()
     rows = torch.empty((N, L), dtype=torch.int32, device=dev)
     out = torch.empty(L, dtype=torch.int32, device=dev)
-    per_round, per_round_graph, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], [], True, [], [], [], [], []
+    per_round, ok_all, Ks, Ds, oks, cm_ms, cm_words = [], True, [], [], [], [], []
+    parity = []
     cm_steady = None
     rec_seq, rec_ovl, rec_cu, rec_q, rec_s, rec_ok = [], [], [], [], [], True
     rep_ms, fp_ovl, fp_q, fp_s = [], [], [], []
@@ -551,24 +643,16 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         torch.cuda.synchronize()
         per_round.append(e0.elapsed_time(e1) / steps)
         ok = bool(torch.all(out == len(on)).item())
-        # the same round captured once as a HIP graph, replayed with one launch per round
-        rg = eng.round_graph(r_on, d_s, d_g, out, L=L)
-        out.fill_(0)
-        rg.launch(stream)
-        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        g0.record(stream)
-        for _ in range(steps):
-            rg.launch(stream)
-        g1.record(stream)
-        torch.cuda.synchronize()
-        per_round_graph.append(g0.elapsed_time(g1) / steps)
-        ok = ok and bool(torch.all(out == len(on)).item())
-        rg.close()
         if check_oracle:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # checker only
             want = O.aggregate_unmask(r_on.cpu().numpy().view(np.uint32), ss, sg, threads=8)
             ok = ok and bool(np.array_equal(want, out.cpu().numpy().view(np.uint32)))
+        elif it == 1 or it == rounds:
+            # windows of the timed round's output against the C oracle (first and last iteration)
+            w = oracle_windows(torch, None, r_on, out, 0, 1, 0, ss, sg, L, None, n=min(L, 2048))
+            parity.append(w["match"])
+            ok = ok and w["match"]
         ok_all &= ok
         if recovery:
             rt = {k: torch.from_numpy(R[k]).to(dev) for k in ("lambdas", "mi_shares", "c1", "pair_shares",
@@ -586,6 +670,12 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
                 torch.cuda.synchronize()
                 acc.append(q0.elapsed_time(q1) / max(2, steps // 4))
                 rec_ok &= bool(torch.all(out == len(on)).item())
+                if it == 1 and rc is recon_q:
+                    # the reconstruction from shares, windows against the oracle given the round's
+                    # own server seeds (what the recovery must have produced)
+                    w = oracle_windows(torch, None, r_on, out, 0, 1, 0, ss, sg, L, None)
+                    parity.append(w["match"])
+                    rec_ok &= w["match"]
             # the reference's own split: S = sum of the rows at report time (:346-350), before any
             # share exists; reconstruction_process then only adds the masks to S (:529-605).  The
             # latency from the shares to final_sum is the same schedules run over the one row S.
@@ -617,7 +707,6 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
         oks.append(int(len(on)))
         del r_on
     ms = float(np.mean(per_round))
-    msg = float(np.mean(per_round_graph))
     nu = float(np.mean(oks))
     extra = {}
     if recovery:
@@ -651,10 +740,13 @@ def measure_config(eng, torch, P, name, N, L, o, dropout, rounds=1, steps=20, ch
     return {"clients": N, "L": L, "neighborhood": o, "dropout": dropout, "iterations": rounds,
             "online_mean": nu, "seeds_K_mean": float(np.mean(Ks)), "dropout_pairs_D_mean": float(np.mean(Ds)),
             "ms_per_round": round(ms, 4), "GB/s": round((4.0 * nu * L + 4.0 * L) / (ms * 1e-3) / 1e9, 1),
-            "graph": {"what": "the same round captured as a HIP graph (flm_round_graph_create), one "
-                              "hipGraphLaunch per round", "ms_per_round": round(msg, 4),
-                      "GB/s": round((4.0 * nu * L + 4.0 * L) / (msg * 1e-3) / 1e9, 1)},
-            "correct": ok_all, "checked_against_oracle": bool(check_oracle),
+            "correct": ok_all,
+            "checked_against_oracle": bool(check_oracle or (parity and all(parity))),
+            "oracle_check": ("the whole output of every iteration against oracle/flamingo_oracle.c" if check_oracle
+                             else f"{len(parity)} checks: the first and last 2048 slots of the output (first and "
+                                  "last iteration" + (", and the first iteration's reconstruction from shares"
+                                                      if recovery else "") + ") against oracle/flamingo_oracle.c, "
+                                  "bit-exact, outside the timed region"),
             "client_masks": {"what": "all N clients' masked vectors y_i = 1 + PRG(m_i) +- PRG(s_ij) "
                                      "(SA_ClientAgent.py:246-324), one flm_client_mask_dev launch",
                              "ms": round(float(np.mean(cm_ms)), 4), "mask_words": int(np.mean(cm_words)),
@@ -940,7 +1032,7 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
     if G >= 8 and eng.cu_count() >= 64:
         rec_cu = ShardedReconstruction(eng, L, comm=rec.comm, ec_cus=int(round(RANK_EC_FRAC * eng.cu_count() / 8)) * 8)
     out = torch.empty(rec.S, dtype=torch.int32, device=dev)
-    per_round, oks, Ds = [], True, []
+    per_round, oks, Ds, parity = [], True, [], []
     rep_ms, fp_ms, fp_cu_ms = [], [], []
     S_shard = torch.empty(rec.S, dtype=torch.int32, device=dev)
     cache = {}
@@ -994,11 +1086,20 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         per_round.append(float(el.item()) / steps * 1e3)
         oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
+        if it == 1:
+            # windows of every rank's shard against the oracle (row sums all-reduced over the ranks)
+            w = oracle_windows(torch, dist, rows, out, rec.lo, G, rank, R["server_seeds"], R["server_signs"], L,
+                               coll)
+            parity.append(w["match"])
         # the reference's split: S shards at report time, then shares -> final over them
         rep_ms.append(timed(lambda: rec.report(rows, S_shard, stream=stream)))
         out.fill_(0)
         fp_ms.append(timed(lambda: rec.run_from_partial(S_shard, *args[1:], stream=stream)))
         oks &= bool(torch.all(out[: rec.hi - rec.lo] == len(on)).item())
+        if it == rounds:
+            w = oracle_windows(torch, dist, rows, out, rec.lo, G, rank, R["server_seeds"], R["server_signs"], L,
+                               coll)
+            parity.append(w["match"])
         if rec_cu is not None:
             out.fill_(0)
             fp_cu_ms.append(timed(lambda: rec_cu.run_from_partial(S_shard, *args[1:], stream=stream)))
@@ -1022,7 +1123,11 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
                                         "what_ec_cus": "the same with the combine on its own first ec_cus CUs and "
                                                        "Shamir + self masks on the rest (dist_recon ec_cus)"}
                                        if rec_cu is not None else {})},
-            "correct": bool(okt.item()),
+            "correct": bool(okt.item()) and all(parity),
+            "checked_against_oracle": bool(parity) and all(parity),
+            "oracle_check": "the first and last 1024 slots of every rank's shard (run of iteration 1, "
+                            f"run_from_partial of iteration {rounds}) against oracle/flamingo_oracle.c given the "
+                            "round's server seeds, row sums all-reduced over the ranks; bit-exact",
             "schedule": "per rank: Shamir of all m_i; EC combine of its ceil(D/G) pair chunk on a side stream under "
                         "rows + self masks over its slot shard; all-gather of the pair keys; pair masks over its "
                         "shard; reduce-scatter ("
@@ -1065,9 +1170,21 @@ def committed_traffic(rows, L, K):
     return best
 
 
-def variant_pairs_only(eng, torch, rows, m, nbrs, online, L, stream, P):
-    """Aggregate + dropout-pair unmask only (K = D), the HBM-bound half of the round."""
-    N = rows.shape[0]
+def gather_full_out(torch, dist, out_mine, S, L, G, coll_dev):
+    """Every rank's output shard (out_mine: slots [lo, hi) of this rank) assembled into the whole
+    uint32[L] vector on every rank (one all-gather of S words per rank; outside the timed region)."""
+    buf = torch.zeros(S, dtype=torch.int32, device=coll_dev)
+    buf[: out_mine.shape[0]] = out_mine.to(coll_dev)
+    parts = [torch.empty_like(buf) for _ in range(G)]
+    dist.all_gather(parts, buf)
+    return torch.cat(parts)[:L].cpu().numpy().view(np.uint32)
+
+
+def variant_pairs_only(eng, torch, rows, nbrs, N, L, stream, P, lo=0, hi=None):
+    """Aggregate + dropout-pair unmask only (K = D), the HBM-bound half of the round: this rank's
+    rows over all L slots plus the pair masks of a 1 % offline set of the N clients over its slot
+    shard [lo, hi) (the whole vector on one GPU)."""
+    hi = L if hi is None else hi
     g = np.random.Generator(np.random.PCG64(99))
     off = np.sort(g.choice(N, max(1, N // 100), replace=False))
     on = np.setdiff1d(np.arange(N), off)
@@ -1081,17 +1198,18 @@ def variant_pairs_only(eng, torch, rows, m, nbrs, online, L, stream, P):
     for name, rr in (("pairs_only", rows),):
         eng.seed_table_dev(d_seeds, d_signs, stream=stream)
         for _ in range(10):
-            eng.aggregate_dev(rr, K, out, L=L, stream=stream)
+            eng.aggregate_dev(rr, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=stream)
         reps = 20
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         ev[0].record(stream)
         for i in range(reps):
-            eng.aggregate_dev(rr, K, out, L=L, stream=stream)
+            eng.aggregate_dev(rr, K, out, L=L, mask_lo=lo, mask_hi=hi, stream=stream)
             ev[i + 1].record(stream)
         torch.cuda.synchronize()
         ms = float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]))   # per launch, median
         gbs = (4.0 * rr.shape[0] * L + 4.0 * L) / (ms * 1e-3) / 1e9
-        res[name] = {"rows": int(rr.shape[0]), "seeds_K": int(K), "kernel_ms": round(ms, 4), "GB/s": round(gbs, 1),
+        res[name] = {"rows": int(rr.shape[0]), "seeds_K": int(K), "mask_slots": [int(lo), int(hi)],
+                     "kernel_ms": round(ms, 4), "GB/s": round(gbs, 1),
                      "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                      "note": "rows summed + dropout-pair masks only (self masks excluded): HBM-bound half"}
     return res
@@ -1189,7 +1307,8 @@ def host_threads():
 
 
 def cpu_baseline(rows, seeds, signs, L, gpu_out):
-    """CPU baseline on this host, same inputs, also cross-checking the GPU bit for bit.
+    """CPU baseline on this host, same inputs, also cross-checking the GPU bit for bit (gpu_out: the
+    GPU's whole output, a device tensor or, at G > 1, the uint32 vector gathered from the ranks).
 
     value: oracle/ref_numpy.py -- the reference's server loop as written there (numpy uint32
     accumulate, one ChaCha20 keystream + frombuffer + temporary per seed), over OpenSSL's C
@@ -1200,7 +1319,7 @@ def cpu_baseline(rows, seeds, signs, L, gpu_out):
     import ref_numpy as R
     N = rows.shape[0]
     host = rows.cpu().numpy().view(np.uint32)
-    gpu = gpu_out.cpu().numpy().view(np.uint32)
+    gpu = gpu_out.cpu().numpy().view(np.uint32) if hasattr(gpu_out, "cpu") else np.asarray(gpu_out, np.uint32)
     bytes_round = 4.0 * N * L + 4.0 * L
     neg = signs < 0
     assert neg.all(), "c4 baseline round has self masks only"

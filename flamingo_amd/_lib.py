@@ -52,9 +52,6 @@ SIGNATURES = {
     "flm_shamir_combine_dev": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
     "flm_pair_units_dev": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp, _int, _int, _vp]),
     "flm_flag_set_dev": (_int, [_vp, _vp, _vp]),
-    "flm_round_graph_create": (_int, [_vp, _vp, _sz, _int, _vp, _vp, _int, _sz, _sz, _sz, _u64, _vp, _vp]),
-    "flm_round_graph_launch": (_int, [_vp, _vp, _vp]),
-    "flm_round_graph_destroy": (_int, [_vp, _vp]),
     "flm_cu_count": (_int, [_vp, _vp]),
     "flm_stream_create_cu_mask": (_int, [_vp, _vp, _int, _vp]),
     "flm_stream_destroy": (_int, [_vp, _vp]),
@@ -71,6 +68,8 @@ SIGNATURES = {
     "flm_group_last_error": (ctypes.c_char_p, [_vp]),
     "flm_group_size": (_int, [_vp]),
     "flm_group_is_loopback": (_int, [_vp]),
+    "flm_group_init_flags": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int), ctypes.c_uint]),
+    "flm_group_has_rccl": (_int, [_vp]),
     "flm_group_ctx": (_vp, [_vp, _int]),
     "flm_group_sync": (_int, [_vp]),
     "flm_group_aggregate_unmask": (_int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),

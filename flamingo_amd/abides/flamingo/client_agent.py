@@ -36,6 +36,23 @@ from .service_agent import SA_ServiceAgent as ServiceAgent
 _MASK128 = (1 << 128) - 1
 
 
+
+def pair_prf(engine, keys, iteration: int) -> list:
+    """h_ijt for every pair key r_ij, as the decimal strings the client hashes to the curve
+    (SA_ClientAgent.py:276-283): str(int.from_bytes(ChaCha20(r_ij, nonce).encrypt(t.to_bytes(16,
+    'big'))[0:4], 'big') & 0xFFFF).  Bytes 0-3 of that ciphertext are keystream word 0 XOR t's
+    first four bytes, so one batched GPU PRG call over all keys gives them: PRG word 0 of a key is
+    LE32(keystream[0:4]) ^ "abcd" (util/param.py:12,32)."""
+    if not keys:
+        return []
+    rnd = int(iteration).to_bytes(16, "big")[:4]
+    ks0 = engine.prg_expand(list(keys), 1)[:, 0] ^ np.uint32(0x64636261)
+    out = []
+    for w in ks0:
+        h = bytes(a ^ b for a, b in zip(int(w).to_bytes(4, "little"), rnd))
+        out.append(str(int.from_bytes(h, "big") & 0xFFFF))
+    return out
+
 class SA_ClientAgent(Agent):
     def __str__(self):
         return "[client]"
@@ -172,11 +189,9 @@ class SA_ClientAgent(Agent):
             enc_mi_shares.append((ct, nonce))
 
         # pairwise seeds: h_ijt -> H (group element) -> s_ij (:266-292)
-        rnd = self.current_iteration.to_bytes(16, "big")
         H, seeds, signs = {}, [mi_bytes], [1]
-        for j in nb:
-            h = C.chacha20_encrypt(self.pair_keys[j], rnd, param.nonce)
-            H[j] = param.hash_to_curve(str(int.from_bytes(h[:4], "big") & 0xFFFF))
+        for j, h in zip(nb, pair_prf(param.engine(), [self.pair_keys[j] for j in nb], self.current_iteration)):
+            H[j] = param.hash_to_curve(h)
             seeds.append(hashlib.sha256(C.point_bytes(H[j])).digest()[: self.key_length])
             signs.append(1 if self.id < j else -1)
 

@@ -84,22 +84,33 @@ def server_devices() -> list:
     return [int(os.environ.get("FLM_DEVICE", "0"))]
 
 
+def server_group_rccl() -> bool:
+    """FLM_GROUP_RCCL=1: a one-device server group still gets an RCCL clique (flm_group_init_flags
+    with FLM_GROUP_RCCL), so the drop-in server runs the multi-GPU code path on one GPU."""
+    return os.environ.get("FLM_GROUP_RCCL", "").strip() not in ("", "0")
+
+
 def server_engine():
     """The server's partial sum and unmask (SA_ServiceAgent.py:346-350, 529-605) run on every
     device of server_devices(): a DeviceGroup (client-sharded rows, slot-sharded masks, one RCCL
-    reduce-scatter) when that is more than one, else the process MaskEngine.  Should the group
-    not come up (RCCL missing, a device refused), the server says so and stays on one GPU."""
+    reduce-scatter) when that is more than one (or FLM_GROUP_RCCL asks for a one-device clique),
+    else the process MaskEngine.  Should the group not come up (RCCL missing, a device refused),
+    the server says so and stays on one GPU.  A group replaced while a VectorStore still uses it is
+    not closed here: the store keeps it alive until the store itself is closed (the agent swaps its
+    store at the next iteration boundary, SA_ServiceAgent.reconstruction_clear_pool)."""
     global _group
     devs = server_devices()
-    if len(devs) == 1 and devs[0] == int(os.environ.get("FLM_DEVICE", "0")):
+    force = server_group_rccl()
+    if len(devs) == 1 and devs[0] == int(os.environ.get("FLM_DEVICE", "0")) and not force:
         return engine()
-    if _group is None or _group.devices != devs:
+    if _group is None or _group.devices != devs or _group.rccl != force:
         from ...engine import DeviceGroup
         if _group is not None:
-            _group.close()
+            if not _group._stores:
+                _group.close()
             _group = None
         try:
-            _group = DeviceGroup(devs)
+            _group = DeviceGroup(devs, force_rccl=force)
         except RuntimeError as e:
             import warnings
             warnings.warn(f"server device group {devs} unavailable ({e}); using one GPU")

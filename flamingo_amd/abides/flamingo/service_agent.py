@@ -134,10 +134,20 @@ class SA_ServiceAgent(Agent):
     @property
     def vec_sum_partial(self) -> np.ndarray:
         """S on the host (copied on demand: the round keeps it on the device between report and
-        reconstruction, :346-350 -> :605)."""
-        if self._store is not None and getattr(self._store, "S", None) is not None:
+        reconstruction, :346-350 -> :605); zeros before the iteration's report, as the reference's
+        attribute reads after its reset (:488-497)."""
+        if self._store is not None and getattr(self._store, "has_partial", False):
             return self._store.host_partial()
         return self._host_partial
+
+    @vec_sum_partial.setter
+    def vec_sum_partial(self, value):
+        """Reference-style assignment (e.g. `server.vec_sum_partial = np.zeros(L, uint32)` before
+        reconstruction_process) sets the host copy the getter returns until the next report."""
+        if self._store is not None and getattr(self._store, "has_partial", False):
+            raise RuntimeError("vec_sum_partial is device-resident after report; assign it before report "
+                               "or after the iteration's reset")
+        self._host_partial = np.asarray(value, dtype=self.vector_dtype)
 
     # ---------------------------------------------------------------- round
     def initialize(self, currentTime):
@@ -264,6 +274,12 @@ class SA_ServiceAgent(Agent):
         self.recv_pairwise_cipher, self.recv_mi_cipher, self.recv_user_vectors = {}, {}, {}
         if self._store is not None:
             self._store.reset()
+            # the server's devices may have changed (FLM_GPUS / FLM_GROUP_DEVICES / FLM_GROUP_RCCL):
+            # a store on the old engine is closed here, between iterations, and made anew on arrival
+            if getattr(self._store, "_owner", None) is not None and self._store._owner is not param.server_engine():
+                self._store.close()
+                self._store = None
+        self._host_partial = np.zeros(self.vector_len, dtype=self.vector_dtype)
         self._accepting = True
 
     def reconstruction_process(self):

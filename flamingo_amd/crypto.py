@@ -57,7 +57,7 @@ def _lib():
         "BN_new": (vp, []), "BN_free": (None, [vp]), "BN_CTX_new": (vp, []),
         "BN_bin2bn": (vp, [ctypes.c_char_p, ip, vp]), "BN_bn2binpad": (ip, [vp, ctypes.c_char_p, ip]),
         "EVP_CIPHER_CTX_new": (vp, []), "EVP_CIPHER_CTX_free": (None, [vp]),
-        "EVP_aes_128_gcm": (vp, []), "EVP_chacha20": (vp, []), "EVP_CIPHER_CTX_ctrl": (ip, [vp, ip, ip, vp]),
+        "EVP_aes_128_gcm": (vp, []), "EVP_CIPHER_CTX_ctrl": (ip, [vp, ip, ip, vp]),
         "EVP_EncryptInit_ex": (ip, [vp, vp, vp, ctypes.c_char_p, ctypes.c_char_p]),
         "EVP_EncryptUpdate": (ip, [vp, ctypes.c_char_p, ctypes.POINTER(ip), ctypes.c_char_p, ip]),
         "EVP_DecryptInit_ex": (ip, [vp, vp, vp, ctypes.c_char_p, ctypes.c_char_p]),
@@ -287,22 +287,6 @@ def aes_gcm_decrypt(key16: bytes, ct: bytes, nonce: bytes) -> bytes:
         n = ctypes.c_int(0)
         assert c.EVP_DecryptUpdate(ctx, out, ctypes.byref(n), ct, len(ct)) == 1
         return out.raw[: n.value]
-    finally:
-        c.EVP_CIPHER_CTX_free(ctx)
-
-
-def chacha20_encrypt(key: bytes, data: bytes, nonce: bytes = bytes(8)) -> bytes:
-    """ChaCha20.new(key=key, nonce=nonce).encrypt(data) for short PRF inputs (h_ijt, SA_ClientAgent.py:276-279).
-    OpenSSL's IV is the 32-bit little-endian block counter then the nonce (12 bytes for the 8-byte DJB nonce)."""
-    c = _lib()
-    ctx = c.EVP_CIPHER_CTX_new()
-    try:
-        iv = bytes(8) + nonce if len(nonce) == 8 else bytes(4) + nonce
-        assert c.EVP_EncryptInit_ex(ctx, c.EVP_chacha20(), None, key, iv) == 1
-        out = ctypes.create_string_buffer(len(data) + 1)
-        n = ctypes.c_int(0)
-        assert c.EVP_EncryptUpdate(ctx, out, ctypes.byref(n), data, len(data)) == 1
-        return out.raw[: len(data)]
     finally:
         c.EVP_CIPHER_CTX_free(ctx)
 

@@ -254,6 +254,7 @@ struct flm_group {
     std::vector<int> dev;
     std::vector<flm_ctx *> ctx;
     bool loopback = false;  // every rank on one device: exchange by shard_sum_kernel, no RCCL
+    bool clique = false;    // RCCL communicators attached (distinct devices; one device with FLM_GROUP_RCCL)
     struct Rank {
         uint32_t *partial = nullptr, *shard = nullptr;
         size_t cap_partial = 0, cap_shard = 0;
@@ -273,6 +274,11 @@ int gfail(flm_group *g, int code, const std::string &msg) {
     flm::rt::set_error(nullptr, code, msg.c_str());
     return code;
 }
+
+// The round goes through partial buffers and an exchange: more than one rank, or a one-device
+// group given a real RCCL clique (FLM_GROUP_RCCL: the 8-GPU code path, collective included, run
+// on one GPU).  Otherwise the one device's round writes its shard -- the whole vector -- directly.
+bool sharded(const flm_group *g) { return g->n > 1 || g->clique; }
 
 int grow(flm_group *g, int r, uint32_t *&p, size_t &cap, size_t words) {
     if (words <= cap) return 0;
@@ -354,11 +360,14 @@ int wait_previous_exchange(flm_group *g, int r) {
 
 extern "C" {
 
-int flm_group_init(flm_group **out, int n, const int *devices) {
+int flm_group_init(flm_group **out, int n, const int *devices) { return flm_group_init_flags(out, n, devices, 0); }
+
+int flm_group_init_flags(flm_group **out, int n, const int *devices, unsigned flags) {
     flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!out) return gfail(nullptr, FLM_EINVAL, "flm_group_init: out is NULL");
     *out = nullptr;
     if (n < 1 || n > flm::kMaxParts) return gfail(nullptr, FLM_EINVAL, "flm_group_init: n must be in [1, 16]");
+    if (flags & ~(unsigned)FLM_GROUP_RCCL) return gfail(nullptr, FLM_EINVAL, "flm_group_init: unknown flags");
     auto *g = new flm_group();
     g->n = n;
     for (int r = 0; r < n; ++r) g->dev.push_back(devices ? devices[r] : r);
@@ -373,6 +382,11 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
         return gfail(nullptr, FLM_EINVAL, "flm_group_init: devices must be all distinct (RCCL) or all equal (loopback)");
     }
     g->loopback = n > 1 && all_same;
+    if (g->loopback && (flags & FLM_GROUP_RCCL)) {  // RCCL refuses two ranks on one device
+        delete g;
+        return gfail(nullptr, FLM_EINVAL, "flm_group_init: FLM_GROUP_RCCL needs distinct devices (RCCL refuses "
+                                          "two ranks on one GPU)");
+    }
     g->rk.resize(n);
     for (int r = 0; r < n; ++r) {
         flm_ctx *c = nullptr;
@@ -389,7 +403,10 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
             return gfail(nullptr, FLM_EHIP, "flm_group_init: hipEventCreate");
         }
     }
-    if (!g->loopback && n > 1) {  // one device needs no communicator: its shard is the whole vector
+    // one device needs no communicator (its shard is the whole vector) unless FLM_GROUP_RCCL asks
+    // for the clique anyway: ncclCommInitAll(1, {dev}) and the grouped reduce-scatter below then
+    // run on a one-GPU box exactly as on the 8-GPU node
+    if (!g->loopback && (n > 1 || (flags & FLM_GROUP_RCCL))) {
         Rccl *r = rccl();
         if (!r) {
             flm_group_free(g);
@@ -408,6 +425,7 @@ int flm_group_init(flm_group **out, int n, const int *devices) {
             cs->rank = q;
             *flm::rt::comm_slot(g->ctx[q]) = cs;
         }
+        g->clique = true;
     }
     *out = g;
     return 0;
@@ -433,6 +451,8 @@ const char *flm_group_last_error(const flm_group *g) { return g ? g->err.c_str()
 int flm_group_size(const flm_group *g) { return g ? g->n : 0; }
 
 int flm_group_is_loopback(const flm_group *g) { return g && g->loopback ? 1 : 0; }
+
+int flm_group_has_rccl(const flm_group *g) { return g && g->clique ? 1 : 0; }
 
 flm_ctx *flm_group_ctx(flm_group *g, int rank) {
     if (!g || rank < 0 || rank >= g->n) return nullptr;
@@ -462,14 +482,15 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
     if (!out || (N > 0 && !rows) || (K > 0 && (!seeds || !signs))) return gfail(g, FLM_EINVAL, "NULL argument");
     int rc_ = 0;
     const int G = g->n;
+    const bool X = sharded(g);
     const uint64_t Lp = padded_len(L, G), S = Lp / G;
     for (int r = 0; r < G; ++r) {
-        if (G > 1 && (rc_ = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp))) return rc_;
+        if (X && (rc_ = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp))) return rc_;
         if ((rc_ = grow(g, r, g->rk[r].shard, g->rk[r].cap_shard, S))) return rc_;
     }
     for (int r = 0; r < G; ++r)
         if ((rc_ = wait_previous_exchange(g, r))) return rc_;
-    for (int r = 0; G > 1 && r < G; ++r)
+    for (int r = 0; X && r < G; ++r)
         if ((rc_ = clear_stale_tail(g, r, L))) return rc_;
     std::vector<int> rcs(G, 0);
     auto work = [&](int r) {
@@ -477,9 +498,9 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         size_t lo, hi;
         flm_client_bounds(N, G, r, &c0, &c1);
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
-        // one device: the round writes its shard (the whole vector) directly, no exchange
+        // one device without a clique: the round writes its shard (the whole vector) directly
         rcs[r] = flm::rt::host_round_async(g->ctx[r], rows ? rows + c0 : nullptr, c1 - c0, seeds, signs, K, L, lo, hi,
-                                           G > 1 ? g->rk[r].partial : g->rk[r].shard);
+                                           X ? g->rk[r].partial : g->rk[r].shard);
         if (!rcs[r] && hipEventRecord(g->rk[r].done, flm::rt::stream_of(g->ctx[r])) != hipSuccess) rcs[r] = FLM_EHIP;
     };
     if (G == 1) {
@@ -493,7 +514,7 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         if (rcs[r]) return rank_error(g, r, rcs[r]);
     std::vector<uint32_t *> shards(G);
     for (int r = 0; r < G; ++r) shards[r] = g->rk[r].shard;
-    if (G > 1 && (rc_ = exchange(g, S, shards))) return rc_;
+    if (X && (rc_ = exchange(g, S, shards))) return rc_;
     for (int r = 0; r < G; ++r) {
         size_t lo, hi;
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
@@ -518,25 +539,26 @@ int flm_group_aggregate_unmask_dev(flm_group *g, const uint32_t *const *d_rows, 
     if (!n_rows || !d_shards || (K > 0 && (!d_seeds || !d_signs))) return gfail(g, FLM_EINVAL, "NULL argument");
     if (L == 0) return 0;
     const int G = g->n;
+    const bool X = sharded(g);
     const uint64_t Lp = padded_len(L, G), S = Lp / G;
-    for (int r = 0; G > 1 && r < G; ++r)
+    for (int r = 0; X && r < G; ++r)
         if (int rc = grow(g, r, g->rk[r].partial, g->rk[r].cap_partial, Lp)) return rc;
     for (int r = 0; r < G; ++r)
         if (int rc = wait_previous_exchange(g, r)) return rc;
-    for (int r = 0; G > 1 && r < G; ++r)
+    for (int r = 0; X && r < G; ++r)
         if (int rc = clear_stale_tail(g, r, L)) return rc;
     for (int r = 0; r < G; ++r) {
         size_t lo, hi;
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
         flm_ctx *c = g->ctx[r];
-        // one device: the round writes the caller's shard (the whole vector) directly
+        // one device without a clique: the round writes the caller's shard (the whole vector) directly
         int rc = flm_aggregate_unmask_dev(c, d_rows ? d_rows[r] : nullptr, row_pitch, n_rows[r],
                                           K ? d_seeds[r] : nullptr, K ? d_signs[r] : nullptr, K, L, lo, hi, 0,
-                                          G > 1 ? g->rk[r].partial : d_shards[r], flm::rt::stream_of(c));
+                                          X ? g->rk[r].partial : d_shards[r], flm::rt::stream_of(c));
         if (rc) return rank_error(g, r, rc);
         if (hipEventRecord(g->rk[r].done, flm::rt::stream_of(c)) != hipSuccess) return gfail(g, FLM_EHIP, "event");
     }
-    if (G == 1) return 0;
+    if (!X) return 0;
     // the exchange writes the caller's shard buffers directly
     return exchange(g, S, std::vector<uint32_t *>(d_shards, d_shards + G));
 }

@@ -399,18 +399,13 @@ int pick_variant(const flm_ctx *ctx, const Plan &plan) {
     return v;
 }
 
-// s == NULL: a synchronous copy (graph capture).  Otherwise the items go through a staging slot
-// on `s` and the plan records `ready` for launches on other streams (run_plan).
-int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items, hipStream_t s = nullptr, bool async = false) {
+// The items go through a staging slot on `s` and the plan records `ready` for launches on
+// other streams (run_plan).
+int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items, hipStream_t s) {
     plan.n_items = (int)items.size();
     if (items.empty()) return 0;
     const size_t bytes = items.size() * sizeof(Item);
     FLM_HIP(ctx, plan.items.reserve(bytes));
-    if (!async) {
-        FLM_HIP(ctx, hipMemcpy(plan.items.p, items.data(), bytes, hipMemcpyHostToDevice));
-        plan.ready_known = true;
-        return 0;
-    }
     int rc = 0;
     StageSlot *slot = stage_acquire(ctx, bytes, &rc);
     if (!slot) return rc;
@@ -571,7 +566,7 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
     Plan *plan = new Plan();
     build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items,
                           *plan, ctx->tune_min_items);
-    *rc = upload_plan(ctx, *plan, items, s, /*async=*/true);
+    *rc = upload_plan(ctx, *plan, items, s);
     if (*rc) { plan_free(plan); return nullptr; }
     if (ctx->plans.size() > 64) {  // bound the cache (hipFree waits for the launches still reading them)
         for (auto &kv : ctx->plans) plan_free(kv.second);
@@ -888,7 +883,7 @@ int flm_device_count(void) {
     return n;
 }
 
-const char *flm_version(void) { return "flamingo_hip 0.1 gfx950 items_kernel<S={1,4,16}>"; }
+const char *flm_version(void) { return "flamingo_hip 0.2 gfx950 items_kernel<S={1,4,16}>"; }
 
 int flm_init(flm_ctx **out, int device) {
     if (!out) return fail(nullptr, FLM_EINVAL, "flm_init: out is NULL");
@@ -1039,100 +1034,6 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
     if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, plan->needs_zero ? d_out : nullptr, L))) return rc;
     return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s, plan->needs_zero);
-}
-
-// A whole device-resident round captured once as a HIP graph: seed schedule,
-// zero-fill (when the plan uses atomics) and the items launch replay with one
-// hipGraphLaunch.  The graph owns its plan, seed table and meta buffers, so the
-// context's caches may be evicted or regrown while it lives; the caller keeps
-// rows/seeds/signs/out alive and may rewrite their contents between launches.
-struct flm_round_graph {
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    DevBuf recs, meta;
-    Plan plan;
-    void destroy() {
-        if (exec) (void)hipGraphExecDestroy(exec);
-        if (graph) (void)hipGraphDestroy(graph);
-        exec = nullptr;
-        graph = nullptr;
-        recs.release();
-        meta.release();
-        plan.items.release();
-    }
-};
-
-int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
-                           const int8_t *d_signs, int K, size_t L, size_t mask_lo, size_t mask_hi, uint64_t prg_slot0,
-                           uint32_t *d_out, void **graph_out) {
-    if (!ctx || !graph_out) return fail(ctx, FLM_EINVAL, "NULL argument");
-    *graph_out = nullptr;
-    if (L == 0) return fail(ctx, FLM_EINVAL, "L must be > 0");
-    if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
-    if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
-    FLM_ON_DEVICE(ctx);
-    auto *g = new flm_round_graph();
-    hipStream_t cs = nullptr;
-    bool capturing = false;
-    auto bail = [&](int code) {
-        if (capturing) {
-            hipGraph_t junk = nullptr;
-            (void)hipStreamEndCapture(cs, &junk);
-            if (junk) (void)hipGraphDestroy(junk);
-        }
-        if (cs) (void)hipStreamDestroy(cs);
-        g->destroy();
-        delete g;
-        return code;
-    };
-    const int B = small_round_width(ctx, N, K, L, mask_lo, mask_hi);
-    std::vector<Item> items;
-    if (!B) {
-        build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0,
-                              items, g->plan, ctx->tune_min_items);
-        if (int rc = upload_plan(ctx, g->plan, items)) return bail(rc);
-    }
-    hipError_t e = g->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec));
-    if (e == hipSuccess)
-        e = g->meta.reserve(sizeof(uint32_t) *
-                            (2 + 2 * (size_t)flm::seed_schedule_groups(K, g->plan.needs_zero ? L : 0)));
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-    capturing = e == hipSuccess;
-    if (e == hipSuccess && B)
-        e = flm::launch_small_round(B, d_rows, row_pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi,
-                                    (uint32_t)(prg_slot0 / 16), d_out, g->meta.as<uint32_t>(), cs);
-    if (e == hipSuccess && !B)
-        e = flm::launch_seed_schedule(d_seeds, d_signs, K, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), cs,
-                                      g->plan.needs_zero ? d_out : nullptr, L);
-    if (e == hipSuccess && !B)
-        e = flm::launch_items(g->plan.subtiles, pick_variant(ctx, g->plan), g->plan.items.as<Item>(), g->plan.n_items,
-                              d_rows, row_pitch, g->recs.as<SeedRec>(), g->meta.as<uint32_t>(), d_out, cs);
-    if (e == hipSuccess) {
-        capturing = false;
-        e = hipStreamEndCapture(cs, &g->graph);
-    }
-    if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
-    if (e != hipSuccess) return bail(fail(ctx, FLM_EHIP, "round graph capture: %s", hipGetErrorString(e)));
-    (void)hipStreamDestroy(cs);
-    *graph_out = g;
-    return 0;
-}
-
-int flm_round_graph_launch(flm_ctx *ctx, void *graph, void *stream) {
-    if (!ctx || !graph) return fail(ctx, FLM_EINVAL, "NULL argument");
-    auto *g = static_cast<flm_round_graph *>(graph);
-    FLM_HIP(ctx, hipGraphLaunch(g->exec, static_cast<hipStream_t>(stream)));
-    return 0;
-}
-
-int flm_round_graph_destroy(flm_ctx *ctx, void *graph) {
-    if (!ctx || !graph) return fail(ctx, FLM_EINVAL, "NULL argument");
-    auto *g = static_cast<flm_round_graph *>(graph);
-    FLM_ON_DEVICE(ctx);
-    g->destroy();
-    delete g;
-    return 0;
 }
 
 int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,

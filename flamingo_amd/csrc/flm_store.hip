@@ -53,6 +53,7 @@ struct StoreRank {
 
 struct flm_store {
     flm_group *group = nullptr;
+    bool via_group = false;      // partial sums through the group's sharded round (G > 1, or an RCCL clique)
     size_t L = 0, pitch = 0, S = 0;
     std::vector<StoreRank> rk;
     std::unordered_map<int64_t, std::pair<int, int>> slot;
@@ -141,17 +142,19 @@ int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int 
     st->L = L;
     st->pitch = (L + 63) / 64 * 64;  // rows 256-B aligned, pitch a multiple of 4 words
     const int G = g ? flm_group_size(g) : 1;
+    // a one-device group with an RCCL clique (FLM_GROUP_RCCL) goes through the group's round too
+    st->via_group = g && (G > 1 || flm_group_has_rccl(g));
     size_t lo = 0, hi = L, S = st->pitch;
     st->rk.resize(G);
     for (int r = 0; r < G; ++r) {
         StoreRank &k = st->rk[r];
         k.ctx = g ? flm_group_ctx(g, r) : ctx;
         k.device = flm::rt::device_of(k.ctx);
-        if (G > 1) flm_shard_bounds(L, G, r, &lo, &hi, &S);
+        if (st->via_group) flm_shard_bounds(L, G, r, &lo, &hi, &S);
         k.lo = lo;
         k.hi = hi;
     }
-    st->S = G > 1 ? S : st->pitch;
+    st->S = st->via_group ? S : st->pitch;
     int rc = 0;
     const int per = std::max(1, (capacity + G - 1) / G);
     for (int r = 0; r < G && !rc; ++r) {
@@ -216,6 +219,12 @@ int flm_store_add(flm_store *st, int64_t sender, const uint32_t *row, size_t n) 
     }
     StoreRank &k = st->rk[r];
     FLM_SHIP(st, hipSetDevice(k.device));
+    if (k.consumed_pending) {
+        // an add between flm_store_partial and flm_store_reset (a late VECTOR the caller forwards
+        // anyway) may overwrite a row the partial sum is still reading: the upload waits for it
+        FLM_SHIP(st, hipStreamWaitEvent(k.copy, k.consumed, 0));
+        k.consumed_pending = false;
+    }
     const int b = k.next;
     k.next = (b + 1) % kStoreRing;
     if (k.stage_busy[b]) FLM_SHIP(st, hipEventSynchronize(k.stage_done[b]));  // its last DMA has read it
@@ -239,7 +248,7 @@ int flm_store_partial(flm_store *st) {
         FLM_SHIP(st, hipEventRecord(k.uploaded, k.copy));
         FLM_SHIP(st, hipStreamWaitEvent(flm::rt::stream_of(k.ctx), k.uploaded, 0));
     }
-    if (G == 1) {
+    if (!st->via_group) {
         StoreRank &k = st->rk[0];
         hipStream_t s = flm::rt::stream_of(k.ctx);
         if (k.n) {

@@ -55,21 +55,29 @@ class ShardedReconstruction:
     EC CUs (tools/probes/rank8_overlap_probe.py, profiles/r03_rank8_overlap_*.log; 64 and 80 CUs
     came out bimodal there).  At G = 4 / 2 the self-mask pass on the remaining CUs is the longer leg
     and the partitioned schedule loses (1.75 -> 2.21 ms, 3.01 -> 4.07 ms; r03_rank_overlap_G{4,2}.log).
-    Default 0: unpartitioned."""
+    Default 0: unpartitioned.
+
+    force_collective: at world 1 run both exchanges through the collective anyway (the library's RCCL
+    communicator when init_rccl attached one, else torch.distributed) instead of the world-1 copies,
+    so a one-GPU box executes the exact code the G-GPU run takes."""
 
     def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None, ec_cus: int = 0,
-                 cu_pick: str = "first"):
+                 cu_pick: str = "first", force_collective: bool = False):
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.force_collective = bool(force_collective)
+        if self.force_collective and not dist.is_initialized():
+            raise RuntimeError("force_collective needs an initialised torch.distributed group")
         self.L = L
         self.Lp = padded_length(L, self.world)
         self.S = self.Lp // self.world
         self.lo, self.hi = shard_bounds(L, self.world, self.rank)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         if comm is None:
-            comm = "rccl" if (self.world > 1 and engine.comm_size() == (self.world, self.rank)) else "torch"
+            comm = "rccl" if ((self.world > 1 or self.force_collective) and engine.has_comm()
+                              and engine.comm_size() == (self.world, self.rank)) else "torch"
         self.comm = comm
         self.ec_cus = int(ec_cus)
         self.pass_stream = None
@@ -109,7 +117,7 @@ class ShardedReconstruction:
             main.wait_event(ev)
 
     def _all_gather(self, chunk, gathered, stream):
-        if self.world == 1:
+        if self.world == 1 and not self.force_collective:
             with torch.cuda.stream(stream):             # torch copies run on the CURRENT stream
                 gathered[: chunk.shape[0]].copy_(chunk)
         elif self.comm == "rccl":
@@ -124,7 +132,7 @@ class ShardedReconstruction:
                     dist.all_gather_into_tensor(gathered, chunk, group=self.group)
 
     def _reduce_scatter(self, part, out, stream):
-        if self.world == 1:
+        if self.world == 1 and not self.force_collective:
             with torch.cuda.stream(stream):
                 out[: self.L].copy_(part[: self.L])
         elif self.comm == "rccl":

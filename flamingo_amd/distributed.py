@@ -107,13 +107,21 @@ class ShardedRound:
     kernel writes the other partial buffer, so round k's collective over xGMI runs under
     round k+1's kernel; a buffer is reused only after the collective that read it has
     completed (a stream-side wait, the host never blocks).  On the RCCL path the
-    collective runs on a comm stream of its own, ordered after the kernel by an event."""
+    collective runs on a comm stream of its own, ordered after the kernel by an event.
 
-    def __init__(self, engine, L: int, group=None, device=None, buffers: int = 1, comm: str | None = None):
+    force_collective: at world 1 reduce-scatter anyway (and pipeline it with buffers=2) instead of
+    returning the partial, so a one-GPU box runs the multi-GPU exchange code."""
+
+    def __init__(self, engine, L: int, group=None, device=None, buffers: int = 1, comm: str | None = None,
+                 force_collective: bool = False):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.force_collective = bool(force_collective)
+        if self.force_collective and not dist.is_initialized():
+            raise RuntimeError("force_collective needs an initialised torch.distributed group")
+        self._solo = self.world == 1 and not self.force_collective    # world 1: the partial is the result
         self.L = L
         self.Lp = padded_length(L, self.world)
         self.S = self.Lp // self.world
@@ -122,11 +130,11 @@ class ShardedRound:
         if buffers not in (1, 2):
             raise ValueError("buffers must be 1 or 2")
         if comm is None:
-            comm = "rccl" if (engine is not None and self.world > 1 and engine.comm_size() == (self.world, self.rank)) \
-                else "torch"
+            comm = "rccl" if (engine is not None and not self._solo and engine.has_comm()
+                              and engine.comm_size() == (self.world, self.rank)) else "torch"
         if comm not in ("rccl", "torch"):
             raise ValueError("comm must be 'rccl' or 'torch'")
-        if comm == "rccl" and engine.comm_size() != (self.world, self.rank):
+        if comm == "rccl" and (not engine.has_comm() or engine.comm_size() != (self.world, self.rank)):
             raise RuntimeError("comm='rccl' needs init_rccl(engine, group) first")
         self.comm = comm
         self._partials = [torch.zeros(self.Lp, dtype=torch.int32, device=dev) for _ in range(buffers)]
@@ -158,7 +166,7 @@ class ShardedRound:
 
     def exchange(self, stream=None):
         """The reduce-scatter of the current partial, ordered after the work on `stream`."""
-        if self.world == 1:
+        if self._solo:
             return self.partial[: self.L]
         if self.comm == "rccl":
             self.engine.reduce_scatter_dev(self.partial, self.out, self.S, stream=stream)
@@ -179,7 +187,7 @@ class ShardedRound:
     def _async_ok(self):
         # RCCL (or gloo on host tensors) can leave the collective in flight; the gloo path
         # over a shared GPU (tests only) goes through host copies and stays synchronous
-        if self.world == 1:
+        if self._solo:
             return False
         if self.comm == "rccl":
             return self._comm_stream is not None
@@ -229,6 +237,6 @@ class ShardedRound:
             else:
                 self._pending[b].wait()
             self._pending[b] = None
-        if self.world == 1:
+        if self._solo:
             return self._partials[b][: self.L]
         return self._outs[b][: self.hi - self.lo]

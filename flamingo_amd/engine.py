@@ -164,6 +164,11 @@ class MaskEngine:
         self.lib.flm_comm_size(self.ctx, ctypes.byref(n), ctypes.byref(r))
         return n.value, r.value
 
+    def has_comm(self) -> bool:
+        """True when an RCCL communicator is attached (flm_comm_size returns 0; 1 = none)."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        return self.lib.flm_comm_size(self.ctx, ctypes.byref(n), ctypes.byref(r)) == 0
+
     def reduce_scatter_dev(self, send, recv, recv_words: int | None = None, stream=None):
         """recv[:recv_words] = this rank's slice of sum_ranks(send) as uint32 (ncclUint32, ncclSum)."""
         n = int(recv.numel() if recv_words is None else recv_words)
@@ -304,27 +309,6 @@ class MaskEngine:
         if rc:
             self._check(rc, "flm_aggregate_unmask_dev")
         return out
-
-    def round_graph(self, rows, seeds, signs, out, L: int | None = None, mask_lo: int = 0,
-                    mask_hi: int | None = None, prg_slot0: int = 0) -> "RoundGraph":
-        """Capture aggregate_unmask_dev's round as a HIP graph (flm_round_graph_create): one
-        hipGraphLaunch per replay.  The tensors are kept alive by the returned object."""
-        N = rows.shape[0] if rows is not None else 0
-        L = (rows.shape[1] if N else 0) if L is None else L
-        pitch = _dev_rows(rows, L) if N else 0
-        mask_hi = L if mask_hi is None else mask_hi
-        K = seeds.shape[0] if seeds is not None else 0
-        if K:
-            _dev_bytes(seeds, "seeds", 32, K)
-            _dev_bytes(signs, "signs", 1, K)
-        _dev_bytes(out, "out", 1, L, 4)
-        h = ctypes.c_void_p()
-        rc = self.lib.flm_round_graph_create(
-            self.ctx, ctypes.c_void_p(rows.data_ptr() if N else 0), pitch, N,
-            ctypes.c_void_p(seeds.data_ptr() if K else 0), ctypes.c_void_p(signs.data_ptr() if K else 0), K, L,
-            mask_lo, mask_hi, prg_slot0, ctypes.c_void_p(out.data_ptr()), ctypes.byref(h))
-        self._check(rc, "flm_round_graph_create")
-        return RoundGraph(self, h, (rows, seeds, signs, out))
 
     def seed_table_dev(self, seeds, signs, stream=None):
         """Build the device seed schedule (first of the round's two launches)."""
@@ -537,29 +521,6 @@ class MaskEngine:
         return bad.value
 
 
-class RoundGraph:
-    """A captured device-resident round (see MaskEngine.round_graph)."""
-
-    def __init__(self, eng: MaskEngine, handle, keep):
-        self.eng, self.h, self._keep = eng, handle, keep
-
-    def launch(self, stream=None):
-        self.eng._check(self.eng.lib.flm_round_graph_launch(self.eng.ctx, self.h, self.eng._stream_handle(stream)),
-                        "flm_round_graph_launch")
-        return self._keep[3]
-
-    def close(self):
-        if self.h is not None and self.h.value and self.eng.ctx is not None:
-            self.eng._check(self.eng.lib.flm_round_graph_destroy(self.eng.ctx, self.h), "flm_round_graph_destroy")
-        self.h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
-
-
 class PinnedArena:
     """Page-locked host memory (hipHostMalloc) viewed as numpy arrays.
 
@@ -633,26 +594,34 @@ class DeviceGroup:
     The reference server is a single-threaded DES process (Kernel.py:190-271); a group gives
     its report/reconstruction steps every device: client-sharded upload and row sum,
     slot-sharded unmask, one RCCL reduce-scatter (ncclUint32), shards back to the host.
-    devices: distinct ids (RCCL clique) or one id repeated (loopback ranks on one GPU)."""
+    devices: distinct ids (RCCL clique) or one id repeated (loopback ranks on one GPU).
+    force_rccl: give a one-device group an RCCL clique too (FLM_GROUP_RCCL), so its rounds take
+    the multi-GPU path -- partial buffer, grouped ncclReduceScatter, shard -- on a one-GPU box."""
 
-    def __init__(self, devices):
+    def __init__(self, devices, force_rccl: bool = False):
         self.lib = _lib.load()
         if isinstance(devices, int):
             devices = list(range(devices))
         devices = [int(d) for d in devices]
         arr = (ctypes.c_int * len(devices))(*devices)
         g = ctypes.c_void_p()
-        rc = self.lib.flm_group_init(ctypes.byref(g), len(devices), arr)
+        rc = self.lib.flm_group_init_flags(ctypes.byref(g), len(devices), arr, 1 if force_rccl else 0)
         if rc != 0:
             raise RuntimeError(f"flm_group_init({devices}): {self.lib.flm_group_last_error(None).decode()}")
         self.g = g
         self.devices = devices
         self.n = len(devices)
         self.loopback = bool(self.lib.flm_group_is_loopback(g))
+        self.rccl = bool(self.lib.flm_group_has_rccl(g))
+        self._stores = 0                    # live VectorStores on this group (close() refuses while > 0)
         self.engines = [MaskEngine(d, _ctx=self.lib.flm_group_ctx(g, r)) for r, d in enumerate(devices)]
 
     def close(self):
+        """Free the group.  Refused while a VectorStore created on it is still open: the store holds
+        the group's contexts and streams (close the stores first)."""
         if getattr(self, "g", None) is not None and self.g.value:
+            if self._stores:
+                raise RuntimeError(f"DeviceGroup.close: {self._stores} VectorStore(s) still use this group")
             for e in self.engines:
                 e.close()
             self.lib.flm_group_free(self.g)

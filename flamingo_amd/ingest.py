@@ -46,6 +46,10 @@ class VectorStore:
             raise RuntimeError(f"flm_store_create: {self.lib.flm_store_last_error(None).decode()}")
         self.h = h
         self.bad = []
+        self.has_partial = False                   # a partial sum S has been enqueued since the last reset
+        self._grp = grp
+        if grp is not None:
+            grp._stores += 1                       # the group refuses to close while its stores are open
 
     def _check(self, rc: int, what: str):
         if rc != 0:
@@ -55,6 +59,8 @@ class VectorStore:
         if getattr(self, "h", None) is not None and self.h.value:
             self.lib.flm_store_free(self.h)
             self.h = None
+            if self._grp is not None:
+                self._grp._stores -= 1
 
     def __del__(self):
         try:
@@ -80,6 +86,7 @@ class VectorStore:
     def reset(self):
         """Forget the stored rows (the next iteration's VECTORs wait for the last partial sum's reads)."""
         self.bad = []
+        self.has_partial = False
         self._check(self.lib.flm_store_reset(self.h), "flm_store_reset")
 
     # ------------------------------------------------------------ the round
@@ -88,6 +95,7 @@ class VectorStore:
         if self.bad:
             raise RuntimeError("Client sends vector of incorrect length.")
         self._check(self.lib.flm_store_partial(self.h), "flm_store_partial")
+        self.has_partial = True
 
     def wait_partial(self) -> float:
         """Block until S is complete; the device time (ms) from partial_sum's call to S done --

@@ -6,7 +6,10 @@ derived exactly as util/param.py:38-112 derives them, but computed once per
 re-derives the whole graph string in every findNeighbors call, :63-76, and
 the server calls it once per offline client, SA_ServiceAgent.py:359-366).
 Every ChaCha20 keystream here is produced on the GPU by the engine
-(``MaskEngine.chacha20_encrypt``); there is no CPU cipher in this package.
+(``MaskEngine.chacha20_encrypt``); the package has no CPU ChaCha20 at all (the
+clients' h_ijt PRF is a GPU batch too, client_agent.py).  The host ciphers it
+does use are OpenSSL's AES-GCM and ECDSA for the m_i shares and signatures
+(flamingo_amd/crypto.py), which are not on the mask path.
 
 The seed tables built here are what the HIP kernels consume:
 * client side (SA_ClientAgent.py:304-324): seeds [m_i, s_ij for j in N(i)]

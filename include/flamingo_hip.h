@@ -176,7 +176,7 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              runs cooperatively.
  *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
  *              per-lane combine kernels (caps their workgroups per CU).
- *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev and flm_round_graph_create run
+ *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev runs
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or
  *              mask_hi == L).  That path builds no device seed table: a following
@@ -249,21 +249,6 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
  * (:397-400) products, n independent elements per call. */
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out);
 
-/* ------------------------------------------------------ captured rounds */
-
-/* One device-resident round (flm_aggregate_unmask_dev's seed schedule,
- * zero-fill and aggregate launch) captured as a HIP graph and replayed with a
- * single hipGraphLaunch: the launch-bound small rounds (BASELINE c2, N=128,
- * L=16384) pay one submission instead of three.  Arguments as
- * flm_aggregate_unmask_dev; the pointers are baked into the graph, so the
- * caller keeps those buffers alive (contents may change between launches).
- * The graph owns its plan and seed table; flm_check_signs does not see it. */
-int flm_round_graph_create(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
-                           const int8_t *d_signs, int K, size_t L, size_t mask_lo, size_t mask_hi, uint64_t prg_slot0,
-                           uint32_t *d_out, void **graph_out);
-int flm_round_graph_launch(flm_ctx *ctx, void *graph, void *stream);
-int flm_round_graph_destroy(flm_ctx *ctx, void *graph);
-
 /* ------------------------------------------------ CU-partitioned streams */
 
 /* A HIP stream whose kernels run only on the CUs set in `mask` (n_words
@@ -323,9 +308,18 @@ int flm_all_gather_dev(flm_ctx *ctx, const void *d_send, void *d_recv, size_t se
  * The rounds run on the ranks' context streams (flm_ctx_stream(flm_group_ctx(g, r))):
  * the caller orders them after the work that produced the inputs.  A group of
  * one device needs no RCCL: its round writes the shard (the whole vector) directly.
- * flm_group_sync waits for every rank's stream. */
+ * flm_group_sync waits for every rank's stream.
+ * flm_group_init_flags(..., FLM_GROUP_RCCL): give the group an RCCL clique even
+ * when it has one device (ncclCommInitAll(1, {dev})); its rounds then take the
+ * multi-GPU path -- partial buffer, grouped ncclReduceScatter, shard -- so the code
+ * the 8-GPU node runs is exercised on a one-GPU box.  Refused for loopback groups
+ * (RCCL does not allow two ranks on one GPU).  flm_group_has_rccl: 1 when the group
+ * has a clique. */
 typedef struct flm_group flm_group;
+#define FLM_GROUP_RCCL 1u
 int flm_group_init(flm_group **out, int n, const int *devices);
+int flm_group_init_flags(flm_group **out, int n, const int *devices, unsigned flags);
+int flm_group_has_rccl(const flm_group *g);
 void flm_group_free(flm_group *g);
 const char *flm_group_last_error(const flm_group *g);
 int flm_group_size(const flm_group *g);

@@ -37,6 +37,7 @@ for _name, _res, _args in (
         ("flm_group_last_error", ctypes.c_char_p, [_vp]),
         ("flm_group_aggregate_unmask", _int, [_vp, ctypes.POINTER(_u32p), _int, _u8p, _i8p, _int, _sz, _u32p]),
         ("flm_store_create", _int, [ctypes.POINTER(_vp), _vp, _vp, _sz, _int]),
+        ("flm_store_free", None, [_vp]),
         ("flm_store_last_error", ctypes.c_char_p, [_vp]),
         ("flm_store_add", _int, [_vp, ctypes.c_int64, _vp, _sz]),
         ("flm_store_partial", _int, [_vp]),
@@ -79,6 +80,17 @@ def _check(rc, group=None):
         raise RuntimeError(msg.decode())
 
 
+def _u32_body(vec, L):
+    """A VECTOR body as contiguous uint32[L], or None when it is not a 1-D 32-bit integer vector of
+    length L: the reference's `vec_sum_partial += v` (SA_ServiceAgent.py:346-350) raises on such a
+    body (wrong length at :348-349; numpy's same-kind cast refuses float and 64-bit bodies), so it
+    is never silently truncated into one."""
+    v = np.asarray(vec)
+    if v.ndim != 1 or v.shape[0] != L or v.dtype.kind not in "ui" or v.dtype.itemsize != 4:
+        return None
+    return np.ascontiguousarray(v).view(np.uint32)
+
+
 def _seed_arrays(seeds, signs):
     K = len(seeds)
     sd = np.frombuffer(b"".join(bytes(s) for s in seeds), np.uint8) if K else np.zeros(32, np.uint8)
@@ -91,10 +103,9 @@ def _seed_arrays(seeds, signs):
 def aggregate_unmask(vectors, seeds, signs, L):
     """sum(vectors) + sum_k signs[k] * PRG(seeds[k]) mod 2^32, as uint32[L]
     (vec_sum_partial + cancel_vec + mi_vec, SA_ServiceAgent.py:346-350, 529-605)."""
-    vecs = [np.ascontiguousarray(v, dtype=np.uint32) for v in vectors]
-    for v in vecs:
-        if v.shape[0] != L:
-            raise RuntimeError("Client sends vector of incorrect length.")
+    vecs = [_u32_body(v, L) for v in vectors]
+    if any(v is None for v in vecs):
+        raise RuntimeError("Client sends vector of incorrect length.")
     rows = (_u32p * max(1, len(vecs)))(*[v.ctypes.data_as(_u32p) for v in vecs])
     sd, sg, K = _seed_arrays(seeds, signs)
     out = np.empty(L, np.uint32)
@@ -172,9 +183,26 @@ class VectorStore:
         if rc:
             raise RuntimeError(_lib.flm_store_last_error(self.h).decode())
 
+    def close(self):
+        """Free the store's device rows and pinned staging ring (flm_store_free)."""
+        if getattr(self, "h", None) is not None and self.h.value:
+            _lib.flm_store_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
     def add(self, sender, vec):
-        v = np.ascontiguousarray(vec, dtype=np.uint32)
-        self._check(_lib.flm_store_add(self.h, int(sender), v.ctypes.data, v.shape[0]))
+        """A body that is not a uint32[L]-compatible vector is remembered as bad: partial() then
+        raises, as report_process does (:348-349)."""
+        v = _u32_body(vec, self.L)
+        if v is None:
+            self._check(_lib.flm_store_add(self.h, int(sender), None, 0))
+            return
+        self._check(_lib.flm_store_add(self.h, int(sender), v.ctypes.data, self.L))
 
     def partial(self):
         """S = sum of the stored vectors, left on the GPU(s); raises on a body of the wrong length

@@ -27,7 +27,7 @@ class OracleStore:
         self.reset()
 
     def reset(self):
-        self.rows, self.bad = {}, []
+        self.rows, self.bad, self.has_partial = {}, [], False
 
     def __len__(self):
         return len(self.rows)
@@ -42,6 +42,7 @@ class OracleStore:
     def partial_sum(self):
         rows = np.stack(list(self.rows.values())) if self.rows else np.zeros((0, self.L), np.uint32)
         self.S = O.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8), L=self.L)
+        self.has_partial = True
 
     def wait_partial(self):
         return 0.0
@@ -74,6 +75,9 @@ class OracleEngine:
 
     def chacha20_encrypt(self, key, data, nonce=bytes(8), counter=0):
         return O.chacha20_encrypt(key, data)
+
+    def prg_expand(self, seeds, L, slot0=0):
+        return np.stack([O.prg(bytes(s), L, slot0) for s in seeds])
 
     def ec_mul_wire(self, points_w, scalars_w):
         pts = C.points_from_wire(points_w)
@@ -133,3 +137,28 @@ def test_wire_formats_roundtrip():
     assert wire.deserialize_dim2_ecp(wire.serialize_dim2_ecp({"a": [E.G]})) == {"a": [E.G]}
     tb = [(b"\x01\x02", b"\xff" * 16)]
     assert wire.deserialize_tuples_bytes(wire.serialize_tuples_bytes(tb)) == tb
+
+
+def test_vec_sum_partial_follows_the_store(oracle_engine):
+    """SA_ServiceAgent.vec_sum_partial (:346-350): zeros before report, S after it (read from the
+    store's has_partial flag, which the real VectorStore carries too), zeros again after the
+    iteration's reset; a reference-style assignment works before report and is refused while S is
+    device-resident."""
+    from flamingo_amd.abides.flamingo.service_agent import SA_ServiceAgent
+    from flamingo_amd.abides.flamingo import protocol
+    protocol.configure(L=64)
+    srv = SA_ServiceAgent(0, "srv", "SA_ServiceAgent", random_state=np.random.RandomState(1), num_clients=4,
+                          users={1, 2, 3})
+    srv.vector_len = 64
+    assert not srv.vec_sum_partial.any()
+    srv.vec_sum_partial = np.full(64, 5, np.uint32)
+    assert np.all(srv.vec_sum_partial == 5)
+    rows = {i: np.full(64, 10 * i, np.uint32) for i in (1, 2, 3)}
+    for i, v in rows.items():
+        srv.store().add(i, v)
+    srv.store().partial_sum()
+    assert np.all(srv.vec_sum_partial == 60)
+    with pytest.raises(RuntimeError, match="device-resident"):
+        srv.vec_sum_partial = np.zeros(64, np.uint32)
+    srv.reconstruction_clear_pool()
+    assert not srv.vec_sum_partial.any()

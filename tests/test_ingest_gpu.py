@@ -23,12 +23,18 @@ def _case(N, K, L, seed):
     return rows, seeds, signs
 
 
-@pytest.mark.parametrize("G", [1, 3])
+@pytest.mark.parametrize("G", [1, "1rccl", 3])
 @pytest.mark.parametrize("N,K,L", [(20, 9, 16000), (7, 0, 4099), (33, 40, 1 << 17)])
 def test_store_round_vs_oracle(G, N, K, L):
+    """G = 1: one engine; 3: loopback ranks; "1rccl": a one-device group with an RCCL clique, whose
+    partial sum takes the group's sharded round and grouped ncclReduceScatter."""
     from flamingo_amd import DeviceGroup, MaskEngine
     from flamingo_amd.ingest import VectorStore
-    eng = MaskEngine(0) if G == 1 else DeviceGroup([0] * G)
+    if G == "1rccl":
+        eng, G = DeviceGroup([0], force_rccl=True), 1
+        assert eng.rccl
+    else:
+        eng = MaskEngine(0) if G == 1 else DeviceGroup([0] * G)
     try:
         st = VectorStore(eng, L, capacity=max(1, N // 2))      # grows past its first capacity
         for it in range(2):                                      # second iteration reuses the rows
@@ -47,6 +53,7 @@ def test_store_round_vs_oracle(G, N, K, L):
             want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
             assert np.array_equal(got, want), (G, N, K, L, it)
             st.reset()
+        st.close()
     finally:
         eng.close()
 
@@ -101,3 +108,37 @@ def test_store_c_abi_checks_lengths_and_reset():
         assert np.array_equal(st.host_partial(), row)
         assert lib.flm_store_unmask(st.h, None, None, -1, ctypes.cast(row.ctypes.data, ctypes.POINTER(ctypes.c_uint32))) != 0
         st.close()
+
+
+def test_store_add_after_partial_waits_for_the_sum():
+    """A sender's row rewritten between flm_store_partial and flm_store_reset (a late VECTOR the
+    reference-side binding forwards, integration/util_flm.py) must not corrupt S: the upload is
+    ordered after the partial sum's reads."""
+    from flamingo_amd import MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    L, N = 1 << 20, 64
+    rows, _, _ = _case(N, 0, L, 5)
+    with MaskEngine(0) as eng:
+        st = VectorStore(eng, L, N)
+        for i in range(N):
+            st.add(i, rows[i])
+        st.partial_sum()
+        for i in range(N):                              # immediately: the sum is still running
+            st.add(i, np.zeros(L, np.uint32))
+        st.wait_partial()
+        assert st.has_partial
+        assert np.array_equal(st.host_partial(), rows.sum(axis=0, dtype=np.uint64).astype(np.uint32))
+        st.reset()
+        assert not st.has_partial
+        st.close()
+
+
+def test_group_close_refused_while_a_store_is_open():
+    from flamingo_amd import DeviceGroup
+    from flamingo_amd.ingest import VectorStore
+    grp = DeviceGroup([0, 0])
+    st = VectorStore(grp, 4096, 2)
+    with pytest.raises(RuntimeError, match="VectorStore"):
+        grp.close()
+    st.close()
+    grp.close()

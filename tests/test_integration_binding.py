@@ -34,8 +34,20 @@ def test_binding_loads_and_binds(monkeypatch):
     flm = load_binding(monkeypatch)
     for name in ("flm_aggregate_unmask", "flm_client_mask", "flm_shamir_combine", "flm_ec_combine",
                  "flm_group_aggregate_unmask", "flm_store_create", "flm_store_add", "flm_store_partial",
-                 "flm_store_unmask", "flm_store_reset"):
+                 "flm_store_unmask", "flm_store_reset", "flm_store_free"):
         assert getattr(flm._lib, name).argtypes
+
+
+def test_binding_body_guard(monkeypatch):
+    """util_flm's VECTOR-body guard (no GPU call): 32-bit integer vectors of length L pass as uint32
+    views; float, 64-bit, 2-D and wrong-length bodies are refused (the reference's uint32 += raises)."""
+    flm = load_binding(monkeypatch)
+    L = 8
+    assert flm._u32_body(np.arange(L, dtype=np.int32), L).dtype == np.uint32
+    assert flm._u32_body(np.arange(L, dtype=np.uint32), L) is not None
+    for bad in (np.arange(L, dtype=np.float32), np.arange(L, dtype=np.int64), np.zeros((2, L), np.uint32),
+                np.arange(L - 1, dtype=np.uint32)):
+        assert flm._u32_body(bad, L) is None
 
 
 @pytest.mark.gpu
@@ -82,3 +94,11 @@ def test_binding_reproduces_reference_round(monkeypatch, ref, refnpz):
     st.add(0, rows[0][:-1])
     with pytest.raises(RuntimeError, match="incorrect length"):
         st.partial()
+    st.reset()
+    st.add(0, rows[0].astype(np.float64))      # the reference's uint32 += refuses it: never truncated
+    with pytest.raises(RuntimeError, match="incorrect length"):
+        st.partial()
+    with pytest.raises(RuntimeError, match="incorrect length"):
+        flm.aggregate_unmask([rows[0].astype(np.float32)], [], [], L)
+    st.close()
+    assert st.h is None

@@ -157,7 +157,7 @@ def test_pair_seed_pipeline_matches_reference(ref, refnpz):
                 k = refnpz[pre + "pair_seg"][i] + c["neighbors"].index(j)
                 rij = hashlib.sha256(C.point_bytes(C.mul(a, C.mul(b)))).digest()
                 assert rij == bytes(r[k])
-                hb = C.chacha20_encrypt(rij, it["iteration"].to_bytes(16, "big"))
+                hb = O.chacha20_encrypt(rij, it["iteration"].to_bytes(16, "big"))
                 h = str(int.from_bytes(hb[:4], "big") & 0xFFFF)
                 assert h == h_ref
                 H = C.hash_str_to_curve(h)
@@ -180,3 +180,20 @@ def test_wire_formats_match_reference_json(ref):
     assert keys == list(d.keys())
     assert [C.point_bytes(v[0]) for v in d.values()] == [bytes(r) for r in c0]
     assert W.wire_to_ecp_json(W.ecp_json_to_wire(w["shared_result_pairwise"])) == w["shared_result_pairwise"]
+
+
+def test_pair_prf_matches_reference_h(ref, refnpz):
+    """The client agent's h_ijt (client_agent.pair_prf: PRG word 0 of each r_ij, one batch, XOR t)
+    against the h_ijt the reference's clients printed (SA_ClientAgent.py:276-283), every pair of
+    run A's two iterations; the PRG here is the C oracle standing in for the GPU."""
+    from flamingo_amd.abides.flamingo.client_agent import pair_prf
+
+    class OraclePRG:
+        def prg_expand(self, seeds, L, slot0=0):
+            return np.stack([O.prg(bytes(x), L, slot0) for x in seeds])
+
+    run = ref["runs"][0]
+    for it in run["iterations"]:
+        r = refnpz[f"{run['name']}_it{it['iteration']}_r"]
+        got = pair_prf(OraclePRG(), [bytes(x) for x in r], it["iteration"])
+        assert got == [h for c in it["clients"] for h in c["h"]], it["iteration"]

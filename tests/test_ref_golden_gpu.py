@@ -117,7 +117,7 @@ def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
     client in every iteration of run 0: public keys b_j G and the ECDH points a_i (b_j G) by the
     batched flm_ec_mul the protocol uses (protocol._ecdh_batch), r_ij = SHA-256 of the point on
     the GPU (flm_ec_combine with no shares: point = c1, seed = SHA-256(c1)), h_ijt from
-    ChaCha20 on the GPU, hash-to-curve on the host, s_ij = SHA-256 on the GPU -- against the
+    ChaCha20 on the GPU (and by the client agent's batched pair_prf), hash-to-curve on the host, s_ij = SHA-256 on the GPU -- against the
     r_ij and s_ij the reference's clients derived from refshim's deterministic pki keys.
     Run D (N = 1024, -o 2: 40k pairs) checks every r_ij and h_ijt, and s_ij on its first n_s
     pairs (hash-to-curve is host Python)."""
@@ -140,6 +140,9 @@ def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
         hs = [str(int.from_bytes(eng.chacha20_encrypt(bytes(x), it["iteration"].to_bytes(16, "big"))[:4], "big")
                   & 0xFFFF) for x in r]
         assert hs == [h for c in it["clients"] for h in c["h"]]
+        # the client agent's own batched form: PRG word 0 of every r_ij in one launch
+        from flamingo_amd.abides.flamingo.client_agent import pair_prf
+        assert pair_prf(eng, [bytes(x) for x in r], it["iteration"]) == hs
         n = len(hs) if n_s is None else min(n_s, len(hs))
         H = np.stack([np.frombuffer(C.point_bytes(C.hash_str_to_curve(h)), np.uint8) for h in hs[:n]])
         _, s, _ = eng.ec_combine_wire(H, none_sh.reshape(0, n, 64), none_l, negate=False)

@@ -2,8 +2,11 @@
 
 Launched by tests/test_distributed_gpu.py with torch.distributed.run on one GPU: gloo ranks sharing
 the card (RCCL refuses duplicate devices) exercise the sharding, the pair-chunk all-gather and the
-reduce-scatter bookkeeping; a one-rank nccl run exercises the library's RCCL communicator
-(flm_all_gather_dev / flm_reduce_scatter_dev).  Every rank checks its own output shard."""
+reduce-scatter bookkeeping.  A one-rank nccl run attaches the library's RCCL communicator and runs
+every case twice: as world 1 normally runs (the exchanges are device copies) and with
+force_collective=True, where both exchanges go through flm_all_gather_dev / flm_reduce_scatter_dev
+(ncclAllGather, ncclReduceScatter on a one-rank communicator) -- the branches the G-GPU run takes.
+Every rank checks its own output shard."""
 import os
 import sys
 
@@ -30,7 +33,10 @@ if backend == "nccl":
     init_rccl(eng)
 dev = torch.device("cuda", 0)
 ok = True
-for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 4)):
+forces = (False, True) if backend == "nccl" and G == 1 else (False,)
+cases = [(N, L, n_off, T, f) for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 4))
+         for f in forces]
+for N, L, n_off, T, force in cases:
     m = np.frombuffer(b"".join(P.bench_seed("dr", i) for i in range(N)), np.uint8).reshape(N, 32)
     nbrs = P.synthetic_neighbors(N, degree=8, seed=N)
     off = np.sort(np.random.Generator(np.random.PCG64(N)).choice(N, n_off, replace=False)) if n_off else \
@@ -46,7 +52,11 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
     D = R["D"]
     a, b, _ = pair_chunk(D, G, r)
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
-    rec = ShardedReconstruction(eng, L)
+    rec = ShardedReconstruction(eng, L, force_collective=force)
+    if backend == "nccl" and (G > 1 or force) and rec.comm != "rccl":
+        print(f"rank {r}: expected the library RCCL communicator, got comm={rec.comm}", flush=True)
+        ok = False
+    tag = f"force_collective={force} comm={rec.comm}"
     out = torch.full((rec.S,), 7, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     for rep in range(2):
@@ -55,7 +65,8 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
         torch.cuda.synchronize()
         got = out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32)
         good = bool(np.all(got == len(on)))
-        print(f"rank {r}/{G} N={N} L={L} D={D} rep {rep}: shard [{rec.lo},{rec.hi}) out==|U| {good}", flush=True)
+        print(f"rank {r}/{G} N={N} L={L} D={D} {tag} rep {rep}: shard [{rec.lo},{rec.hi}) out==|U| {good}",
+              flush=True)
         ok &= good
     # the reference's split: S shards at report, masks over them at reconstruction
     S_shard = torch.full((rec.S,), 5, dtype=torch.int32, device=dev)
@@ -69,10 +80,10 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
                          t(R["pair_signs"]), D, out)
     torch.cuda.synchronize()
     good &= bool(np.all(out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32) == len(on)))
-    print(f"rank {r}/{G} N={N} L={L} D={D} from report partial: S shard and out==|U| {good}", flush=True)
+    print(f"rank {r}/{G} N={N} L={L} D={D} {tag} from report partial: S shard and out==|U| {good}", flush=True)
     ok &= good
     # the CU-partitioned schedule: combine on its own CUs, Shamir + self masks on the rest
-    rec_cu = ShardedReconstruction(eng, L, ec_cus=max(8, eng.cu_count() // 4 // 8 * 8))
+    rec_cu = ShardedReconstruction(eng, L, ec_cus=max(8, eng.cu_count() // 4 // 8 * 8), force_collective=force)
     for name, fn in (("run", lambda: rec_cu.run(r_rows, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]),
                                                 t(R["pair_shares"][:, a:b]), t(R["pair_signs"]), D, out)),
                      ("from report partial", lambda: rec_cu.run_from_partial(
@@ -82,7 +93,7 @@ for N, L, n_off, T in ((256, 20000, 7, 5), (512, 1 << 16, 9, 20), (64, 5000, 0, 
         fn()
         torch.cuda.synchronize()
         good = bool(np.all(out[: rec.hi - rec.lo].cpu().numpy().view(np.uint32) == len(on)))
-        print(f"rank {r}/{G} N={N} L={L} D={D} ec_cus={rec_cu.ec_cus} {name}: out==|U| {good}", flush=True)
+        print(f"rank {r}/{G} N={N} L={L} D={D} {tag} ec_cus={rec_cu.ec_cus} {name}: out==|U| {good}", flush=True)
         ok &= good
 okt = torch.tensor([1 if ok else 0])
 if backend == "nccl":

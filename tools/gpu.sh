@@ -10,6 +10,8 @@
 #   benchG:N     bench.py --gpus N --dist-backend gloo --steps 3 (N self-launched ranks on the one GPU:
 #                the sharded c4 and c5 paths end to end, correctness only)
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
+#   rccl         tools/rccl_clique_smoke.py (forced one-device RCCL clique + world-1 forced collectives),
+#                then the same under rocprofv3 --kernel-trace --memory-copy-trace --stats
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
 #   py:SCRIPT[:ARG]  python tools/SCRIPT [ARG] (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
@@ -48,6 +50,15 @@ for step in "$@"; do
     sim)
       timeout -k 10 300 python -m flamingo_amd.abides -c flamingo -n 128 -i 1 -p 1 > "$O/${TAG}_sim_c1_n128.log" 2>&1 || exit 1
       timeout -k 10 600 python -m flamingo_amd.abides -c flamingo -n 1024 -i 2 -p 1 > "$O/${TAG}_sim_n1024_i2.log" 2>&1 || exit 1 ;;
+    rccl)
+      # every RCCL branch of the multi-GPU path on the one GPU (tools/rccl_clique_smoke.py), then the
+      # same script under a kernel + memory-copy trace: the RCCL kernels / copies it launched
+      timeout -k 10 300 python -u tools/rccl_clique_smoke.py > "$O/${TAG}_rccl_clique.log" 2>&1 \
+        || { tail -30 "$O/${TAG}_rccl_clique.log"; exit 1; }
+      tail -2 "$O/${TAG}_rccl_clique.log"
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+        -d "$O/${TAG}_rccl_trace" -o run -- python3 "$R/tools/rccl_clique_smoke.py" > "$O/${TAG}_rccl_trace.log" 2>&1) \
+        || { tail -20 "$O/${TAG}_rccl_trace.log"; exit 1; } ;;
     prof)
       bash tools/gpu_prof.sh "$TAG" || exit 1 ;;
     clock)

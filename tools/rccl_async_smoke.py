@@ -1,8 +1,10 @@
 """One-rank RCCL run of ShardedRound's pipelined path (buffers=2, async reduce-scatter, stream-side
-waits) on a one-GPU box: with world_size 1 the collective is a copy, but the Work/stream handling
-is exactly the multi-GPU code.  Checks every round's shard against the synchronous round, for both
-exchanges: torch.distributed's reduce-scatter and the library's own communicator
-(init_rccl -> flm_comm_init_rank, flm_reduce_scatter_dev with ncclUint32 on a comm stream)."""
+waits) on a one-GPU box, with force_collective=True so world 1 takes the multi-GPU branches: the
+collective is a copy on one rank, but the Work/stream handling is exactly the multi-GPU code.
+Checks every round's shard against the plain world-1 round (no collective), for both exchanges:
+torch.distributed's reduce-scatter and the library's own communicator (init_rccl ->
+flm_comm_init_rank, flm_reduce_scatter_dev with ncclUint32 on a comm stream); the synchronous
+forced round (buffers=1) too."""
 import os
 import sys
 
@@ -35,8 +37,15 @@ for r in rows:
 torch.cuda.synchronize()
 ok = True
 for comm in ("torch", "rccl"):
-    pipe = ShardedRound(eng, L, buffers=2, comm=comm)
-    pipe._async_ok = lambda: True          # world 1: force the async path
+    sync = ShardedRound(eng, L, comm=comm, force_collective=True)
+    for i, r in enumerate(rows):
+        got = sync.step(r, seeds, signs, stream)
+        torch.cuda.synchronize()
+        e = bool(torch.equal(got[:L], want[i]))
+        print(f"{comm} synchronous forced collective round {i}: out==want {e}", flush=True)
+        ok &= e
+    pipe = ShardedRound(eng, L, buffers=2, comm=comm, force_collective=True)
+    assert pipe._async_ok() and pipe.comm == comm
     with torch.cuda.stream(stream):
         for rep in range(4):
             bufs = [pipe.launch(r, seeds, signs, stream) for r in rows]
@@ -53,8 +62,7 @@ for comm in ("torch", "rccl"):
 # `stream` first so an unordered collective would read a partial before it is written
 side = torch.cuda.Stream()
 for comm in ("torch", "rccl"):
-    pipe = ShardedRound(eng, L, buffers=2, comm=comm)
-    pipe._async_ok = lambda: True
+    pipe = ShardedRound(eng, L, buffers=2, comm=comm, force_collective=True)
     big = torch.randint(0, 100, (4096, 4096), device="cuda", dtype=torch.float32, generator=g)
     with torch.cuda.stream(side):            # current stream: `side`; the round runs on `stream`
         for rep in range(2):
