@@ -24,6 +24,7 @@
 
 #include <cstdint>
 
+#include "flm_fe_row.h"
 #include "flm_internal.h"
 
 namespace flm {
@@ -32,9 +33,11 @@ namespace {
 struct Fe {
     uint32_t v[8];
 };
-struct Jac {
-    Fe X, Y, Z;
+template <class E>
+struct JacT {
+    E X, Y, Z;
 };
+using Jac = JacT<Fe>;
 
 __device__ constexpr uint32_t kP[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u, 1u, 0xffffffffu};
 __device__ constexpr uint32_t kOne[8] = {0x00000001u, 0x00000000u, 0x00000000u, 0xffffffffu,
@@ -1064,13 +1067,72 @@ __device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool n
 #endif  // !FLM_COOP_MODJ
 
 #if FLM_COOP_MODJ
-// ---- modified Jacobian (X, Y, Z, W = Z^4) for the cooperative kernel (FLM_COOP_MODJ, default on)
+// ---- modified Jacobian (X, Y, Z, W = Z^4) for the cooperative kernels (FLM_COOP_MODJ, default on)
 // Carrying W takes the doubling's a Z^4 term off the critical path: alpha = 3 (X^2 - W) needs one
 // squaring, so alpha^2 lands one level earlier and a doubling is 3 multiplications of latency and
 // two barriers instead of 4 and three.  Same outputs as dbl-2001-b (X3, Y3, Z3 are identical), so
 // the Jacobian result and everything after it are bit-identical.
-struct JacW {
-    Fe X, Y, Z, W;
+//
+// The formulas are written once over a field policy F: LaneField (one element per lane, the
+// Montgomery limbs of flm_p256.hip, exchange slots of 512 words) for ec_mul_coop_kernel, and
+// RowField (one element per 16-lane row, flm_fe_row.h, slots of 64 words) for ec_mul_row_kernel.
+template <class E>
+struct JacWT {
+    E X, Y, Z, W;
+};
+using JacW = JacWT<Fe>;
+
+struct LaneField {
+    using E = Fe;
+    static constexpr int kSlot = 512;       // words per exchange slot: 64 lanes x 8 limbs
+    static constexpr int kCoord = 8 * 64;   // words per coordinate of a table entry
+    static constexpr int kEntry = 24 * 64;  // words per table entry (X, Y, Z)
+    __device__ __forceinline__ E mul(const E &a, const E &b) const { return fe_mul(a, b); }
+    __device__ __forceinline__ E sqr(const E &a) const { return fe_sqr(a); }
+    __device__ __forceinline__ E add(const E &a, const E &b) const { return fe_add(a, b); }
+    __device__ __forceinline__ E sub(const E &a, const E &b) const { return fe_sub(a, b); }
+    __device__ __forceinline__ E neg(const E &a) const { return fe_neg(a); }
+    __device__ __forceinline__ bool is_zero(const E &a) const { return fe_is_zero(a); }
+    __device__ __forceinline__ void put(uint32_t *slot, const E &a, int lane) const { xput(slot, a, lane); }
+    __device__ __forceinline__ E get(const uint32_t *slot, int lane) const { return xget(slot, lane); }
+    __device__ __forceinline__ JacT<E> inf() const { return jac_inf(); }
+    __device__ __forceinline__ JacT<E> dbl(const JacT<E> &P) const { return jac_dbl(P); }
+};
+
+struct RowField {
+    using E = uint32_t;
+    static constexpr int kSlot = 64;  // one word per lane: 4 elements x 16 lanes
+    static constexpr int kCoord = 64;
+    static constexpr int kEntry = 3 * 64;
+    row::Ctx K;
+    __device__ __forceinline__ E mul(E a, E b) const { return row::mul(a, b, K); }
+    __device__ __forceinline__ E sqr(E a) const { return row::sqr(a, K); }
+    __device__ __forceinline__ E add(E a, E b) const { return row::add(a, b, K); }
+    __device__ __forceinline__ E sub(E a, E b) const { return row::sub(a, b, K); }
+    __device__ __forceinline__ E neg(E a) const { return row::neg(a, K); }
+    __device__ __forceinline__ bool is_zero(E a) const { return row::is_zero(a, K); }
+    __device__ __forceinline__ void put(uint32_t *slot, E a, int lane) const { slot[lane] = a; }
+    __device__ __forceinline__ E get(const uint32_t *slot, int lane) const { return slot[lane]; }
+    __device__ __forceinline__ E one() const { return (threadIdx.x & 15) == 0 ? 1u : 0u; }
+    __device__ __forceinline__ JacT<E> inf() const {  // (1, 1, 0), normal form
+        JacT<E> r;
+        r.X = r.Y = one();
+        r.Z = 0u;
+        return r;
+    }
+    // dbl-2001-b, as jac_dbl (the rare acc == Q path of an addition)
+    __device__ JacT<E> dbl(const JacT<E> &P) const {
+        const E delta = sqr(P.Z), gamma = sqr(P.Y), beta = mul(P.X, gamma);
+        const E t = mul(sub(P.X, delta), add(P.X, delta));
+        const E alpha = add(add(t, t), t);
+        const E beta4 = add(add(beta, beta), add(beta, beta));
+        JacT<E> R;
+        R.X = sub(sqr(alpha), add(beta4, beta4));
+        R.Z = sub(sub(sqr(add(P.Y, P.Z)), gamma), delta);
+        const E g2 = sqr(gamma), g4 = add(g2, g2), g8 = add(g4, g4);
+        R.Y = sub(mul(alpha, sub(beta4, R.X)), g8);
+        return R;
+    }
 };
 
 //   before barrier 1  w0: XX = X^2, alpha = 3 (XX - W), alpha^2
@@ -1081,171 +1143,177 @@ struct JacW {
 // Slots 0..2 are read by w0 before barrier 2; the results (6..9) are written only between the two
 // barriers, so the next operation's writes before its first barrier (slots 0..2 for a doubling,
 // A/B = 0/1 for an addition) never land on a slot another wave is still reading.
-__device__ __forceinline__ void coop_dbl_w(JacW &acc, int w, int lane, uint32_t *S) {
-    Fe alpha, a2, g8, z3;
+template <class F>
+__device__ __forceinline__ void coop_dbl_w(JacWT<typename F::E> &acc, int w, int lane, uint32_t *S, const F &f) {
+    using E = typename F::E;
+    constexpr int Q = F::kSlot;
+    E alpha, a2, g8, z3;
     if (w == 0) {
-        const Fe t = fe_sub(fe_sqr(acc.X), acc.W);
-        alpha = fe_add(fe_add(t, t), t);
-        a2 = fe_sqr(alpha);
+        const E t = f.sub(f.sqr(acc.X), acc.W);
+        alpha = f.add(f.add(t, t), t);
+        a2 = f.sqr(alpha);
     } else if (w == 1) {
-        const Fe beta = fe_mul(acc.X, fe_sqr(acc.Y));
-        const Fe b2 = fe_add(beta, beta);
-        const Fe b4 = fe_add(b2, b2);
-        xput(S + 0 * 512, b4, lane);
-        xput(S + 1 * 512, fe_add(b4, b4), lane);
+        const E beta = f.mul(acc.X, f.sqr(acc.Y));
+        const E b2 = f.add(beta, beta);
+        const E b4 = f.add(b2, b2);
+        f.put(S + 0 * Q, b4, lane);
+        f.put(S + 1 * Q, f.add(b4, b4), lane);
     } else if (w == 2) {
-        Fe g = fe_sqr(fe_sqr(acc.Y));
-        g = fe_add(g, g);
-        g = fe_add(g, g);
-        g8 = fe_add(g, g);
-        xput(S + 2 * 512, g8, lane);
+        E g = f.sqr(f.sqr(acc.Y));
+        g = f.add(g, g);
+        g = f.add(g, g);
+        g8 = f.add(g, g);
+        f.put(S + 2 * Q, g8, lane);
     } else {
-        const Fe yz = fe_mul(acc.Y, acc.Z);
-        z3 = fe_add(yz, yz);
+        const E yz = f.mul(acc.Y, acc.Z);
+        z3 = f.add(yz, yz);
     }
     __syncthreads();
     if (w == 0) {
-        const Fe x3 = fe_sub(a2, xget(S + 1 * 512, lane));
-        xput(S + 6 * 512, x3, lane);
-        xput(S + 7 * 512, fe_sub(fe_mul(alpha, fe_sub(xget(S + 0 * 512, lane), x3)), xget(S + 2 * 512, lane)), lane);
+        const E x3 = f.sub(a2, f.get(S + 1 * Q, lane));
+        f.put(S + 6 * Q, x3, lane);
+        f.put(S + 7 * Q, f.sub(f.mul(alpha, f.sub(f.get(S + 0 * Q, lane), x3)), f.get(S + 2 * Q, lane)), lane);
     } else if (w == 2) {
-        xput(S + 9 * 512, fe_mul(fe_add(g8, g8), acc.W), lane);
+        f.put(S + 9 * Q, f.mul(f.add(g8, g8), acc.W), lane);
     } else if (w == 3) {
-        xput(S + 8 * 512, z3, lane);
+        f.put(S + 8 * Q, z3, lane);
     }
     __syncthreads();
-    acc.X = xget(S + 6 * 512, lane);
-    acc.Y = xget(S + 7 * 512, lane);
-    acc.Z = xget(S + 8 * 512, lane);
-    acc.W = xget(S + 9 * 512, lane);
+    acc.X = f.get(S + 6 * Q, lane);
+    acc.Y = f.get(S + 7 * Q, lane);
+    acc.Z = f.get(S + 8 * Q, lane);
+    acc.W = f.get(S + 9 * Q, lane);
 }
 
 // coop_add with W carried: the same six levels; w3, idle after L3, squares its Z3 twice (L4, L5)
 // into slot H, and L6 picks W for the exceptional cases (Q or a doubling: two squarings of the new
 // Z on that rare path; infinity: 0; acc: its own W).  Result slots D, E, F and K (W).
-__device__ __forceinline__ void coop_add_w(JacW &acc, bool sel, int tab_idx, bool neg, int w, int lane, uint32_t *S,
-                                           const uint32_t *tab) {
-    const uint32_t *q = tab + (size_t)tab_idx * 24 * 64;
-    Jac Q;
-    Q.X = xget(q, lane);
-    Q.Y = xget(q + 8 * 64, lane);
-    Q.Z = xget(q + 16 * 64, lane);
-    if (neg) Q.Y = fe_neg(Q.Y);
-    uint32_t *A = S, *B = S + 512, *C = S + 2 * 512, *Dd = S + 3 * 512, *E = S + 4 * 512, *F = S + 5 * 512,
-             *G = S + 6 * 512, *H = S + 7 * 512, *I = S + 8 * 512, *J = S + 9 * 512, *K = S + 10 * 512;
-    Fe z1z1, z2z2, zz, s2a, s1a, u1, u2, s2, s1, h, i, j, v, x3, y3a, z3;
+template <class F>
+__device__ __forceinline__ void coop_add_w(JacWT<typename F::E> &acc, bool sel, int tab_idx, bool neg, int w, int lane,
+                                           uint32_t *S, const uint32_t *tab, const F &f) {
+    using E = typename F::E;
+    constexpr int Q_ = F::kSlot;
+    const uint32_t *q = tab + (size_t)tab_idx * F::kEntry;
+    JacT<E> Q;
+    Q.X = f.get(q, lane);
+    Q.Y = f.get(q + F::kCoord, lane);
+    Q.Z = f.get(q + 2 * F::kCoord, lane);
+    if (neg) Q.Y = f.neg(Q.Y);
+    uint32_t *A = S, *B = S + Q_, *C = S + 2 * Q_, *Dd = S + 3 * Q_, *Ee = S + 4 * Q_, *Fs = S + 5 * Q_,
+             *G = S + 6 * Q_, *H = S + 7 * Q_, *I = S + 8 * Q_, *J = S + 9 * Q_, *K = S + 10 * Q_;
+    E z1z1, z2z2, zz, s2a, s1a, u1, u2, s2, s1, h, i, j, v, x3, y3a, z3;
     // L1
     if (w == 0) {
-        z1z1 = fe_sqr(acc.Z);
-        xput(A, z1z1, lane);
+        z1z1 = f.sqr(acc.Z);
+        f.put(A, z1z1, lane);
     } else if (w == 1) {
-        z2z2 = fe_sqr(Q.Z);
-        xput(B, z2z2, lane);
+        z2z2 = f.sqr(Q.Z);
+        f.put(B, z2z2, lane);
     } else if (w == 2) {
-        zz = fe_sqr(fe_add(acc.Z, Q.Z));
+        zz = f.sqr(f.add(acc.Z, Q.Z));
     } else {
-        s1a = fe_mul(acc.Y, Q.Z);
+        s1a = f.mul(acc.Y, Q.Z);
     }
     __syncthreads();
     // L2
     if (w == 0) {
-        xput(Dd, fe_mul(Q.X, z1z1), lane);  // u2
+        f.put(Dd, f.mul(Q.X, z1z1), lane);  // u2
     } else if (w == 1) {
-        u1 = fe_mul(acc.X, z2z2);
-        xput(E, u1, lane);
+        u1 = f.mul(acc.X, z2z2);
+        f.put(Ee, u1, lane);
     } else if (w == 2) {
-        z1z1 = xget(A, lane);
-        z2z2 = xget(B, lane);
-        xput(F, fe_sub(fe_sub(zz, z1z1), z2z2), lane);  // Z3'
-        s2a = fe_mul(Q.Y, acc.Z);
+        z1z1 = f.get(A, lane);
+        z2z2 = f.get(B, lane);
+        f.put(Fs, f.sub(f.sub(zz, z1z1), z2z2), lane);  // Z3'
+        s2a = f.mul(Q.Y, acc.Z);
     } else {
-        z2z2 = xget(B, lane);
-        xput(G, fe_mul(s1a, z2z2), lane);  // s1
+        z2z2 = f.get(B, lane);
+        f.put(G, f.mul(s1a, z2z2), lane);  // s1
     }
     __syncthreads();
     // L3
     if (w == 0) {
-        u2 = xget(Dd, lane);
-        u1 = xget(E, lane);
-        h = fe_sub(u2, u1);
-        const Fe h2 = fe_add(h, h);
-        i = fe_sqr(h2);
-        xput(H, i, lane);
+        u2 = f.get(Dd, lane);
+        u1 = f.get(Ee, lane);
+        h = f.sub(u2, u1);
+        const E h2 = f.add(h, h);
+        i = f.sqr(h2);
+        f.put(H, i, lane);
     } else if (w == 2) {
-        s2 = fe_mul(s2a, z1z1);
+        s2 = f.mul(s2a, z1z1);
     } else if (w == 3) {
-        u2 = xget(Dd, lane);
-        u1 = xget(E, lane);
-        z3 = fe_mul(xget(F, lane), fe_sub(u2, u1));  // Z3 = Z3' h
-        xput(I, z3, lane);
+        u2 = f.get(Dd, lane);
+        u1 = f.get(Ee, lane);
+        z3 = f.mul(f.get(Fs, lane), f.sub(u2, u1));  // Z3 = Z3' h
+        f.put(I, z3, lane);
     }
     __syncthreads();
     // L4
     if (w == 0) {
-        j = fe_mul(h, i);
-        xput(J, j, lane);
+        j = f.mul(h, i);
+        f.put(J, j, lane);
     } else if (w == 1) {
-        i = xget(H, lane);
-        v = fe_mul(u1, i);
-        xput(K, v, lane);
-        xput(Dd, fe_add(v, v), lane);
+        i = f.get(H, lane);
+        v = f.mul(u1, i);
+        f.put(K, v, lane);
+        f.put(Dd, f.add(v, v), lane);
     } else if (w == 2) {
-        s1 = xget(G, lane);
-        Fe r = fe_sub(s2, s1);
-        r = fe_add(r, r);
-        xput(A, r, lane);
-        xput(B, fe_sqr(r), lane);
+        s1 = f.get(G, lane);
+        E r = f.sub(s2, s1);
+        r = f.add(r, r);
+        f.put(A, r, lane);
+        f.put(B, f.sqr(r), lane);
     } else {
-        z3 = fe_sqr(z3);
+        z3 = f.sqr(z3);
     }
     __syncthreads();
     // L5
-    Fe r;
+    E r;
     if (w == 0) {
-        v = xget(K, lane);
-        r = xget(A, lane);
-        const Fe rr = xget(B, lane);
-        x3 = fe_sub(fe_sub(rr, j), xget(Dd, lane));
-        y3a = fe_mul(r, fe_sub(v, x3));
+        v = f.get(K, lane);
+        r = f.get(A, lane);
+        const E rr = f.get(B, lane);
+        x3 = f.sub(f.sub(rr, j), f.get(Dd, lane));
+        y3a = f.mul(r, f.sub(v, x3));
     } else if (w == 1) {
-        s1 = xget(G, lane);
-        j = xget(J, lane);
-        const Fe s1j = fe_mul(s1, j);
-        xput(C, fe_add(s1j, s1j), lane);
+        s1 = f.get(G, lane);
+        j = f.get(J, lane);
+        const E s1j = f.mul(s1, j);
+        f.put(C, f.add(s1j, s1j), lane);
     } else if (w == 3) {
-        xput(H, fe_sqr(z3), lane);  // W3 = Z3^4 (H's i was read at L4)
+        f.put(H, f.sqr(z3), lane);  // W3 = Z3^4 (H's i was read at L4)
     }
     __syncthreads();
     // L6
     if (w == 0) {
-        JacW R;
+        JacWT<E> R;
         R.X = x3;
-        R.Y = fe_sub(y3a, xget(C, lane));
-        R.Z = xget(I, lane);
-        R.W = xget(H, lane);
-        if (fe_is_zero(acc.Z)) {
+        R.Y = f.sub(y3a, f.get(C, lane));
+        R.Z = f.get(I, lane);
+        R.W = f.get(H, lane);
+        if (f.is_zero(acc.Z)) {
             R.X = Q.X; R.Y = Q.Y; R.Z = Q.Z;
-            R.W = fe_sqr(fe_sqr(Q.Z));
-        } else if (fe_is_zero(Q.Z)) {
+            R.W = f.sqr(f.sqr(Q.Z));
+        } else if (f.is_zero(Q.Z)) {
             R = acc;
-        } else if (fe_is_zero(h)) {
-            Jac a;
+        } else if (f.is_zero(h)) {
+            JacT<E> a;
             a.X = acc.X; a.Y = acc.Y; a.Z = acc.Z;
-            const Jac d = fe_is_zero(r) ? jac_dbl(a) : jac_inf();  // acc == Q / acc == -Q (rare: one lane)
+            const JacT<E> d = f.is_zero(r) ? f.dbl(a) : f.inf();  // acc == Q / acc == -Q (rare: one lane)
             R.X = d.X; R.Y = d.Y; R.Z = d.Z;
-            R.W = fe_sqr(fe_sqr(d.Z));
+            R.W = f.sqr(f.sqr(d.Z));
         }
         if (!sel) R = acc;
-        xput(Dd, R.X, lane);
-        xput(E, R.Y, lane);
-        xput(F, R.Z, lane);
-        xput(K, R.W, lane);
+        f.put(Dd, R.X, lane);
+        f.put(Ee, R.Y, lane);
+        f.put(Fs, R.Z, lane);
+        f.put(K, R.W, lane);
     }
     __syncthreads();
-    acc.X = xget(Dd, lane);
-    acc.Y = xget(E, lane);
-    acc.Z = xget(F, lane);
-    acc.W = xget(K, lane);
+    acc.X = f.get(Dd, lane);
+    acc.Y = f.get(Ee, lane);
+    acc.Z = f.get(Fs, lane);
+    acc.W = f.get(K, lane);
 }
 
 #endif  // FLM_COOP_MODJ
@@ -1287,7 +1355,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
     PW.X = P.X; PW.Y = P.Y; PW.Z = P.Z;
     PW.W = fe_sqr(fe_sqr(P.Z));
     JacW P2 = PW;
-    coop_dbl_w(P2, w, lane, S);
+    coop_dbl_w(P2, w, lane, S, LaneField{});
     if (w == 0) {
         xput(tab, P.X, lane);
         xput(tab + 8 * 64, P.Y, lane);
@@ -1300,7 +1368,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
     JacW t = PW;
 #pragma unroll 1
     for (int k = 1; k < 8; ++k) {
-        coop_add_w(t, true, 1, false, w, lane, S, tab);
+        coop_add_w(t, true, 1, false, w, lane, S, tab, LaneField{});
         if (w == 0) {
             uint32_t *q = tab + (size_t)(k == 1 ? 8 : k) * 24 * 64;
             xput(q, t.X, lane);
@@ -1324,9 +1392,9 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
     }
 #pragma unroll 1
     for (int k = kNafLen - 1; k >= 0; --k) {
-        coop_dbl_w(accw, w, lane, S);
+        coop_dbl_w(accw, w, lane, S, LaneField{});
         const int v = dig[k];
-        if (__any(v != 0)) coop_add_w(accw, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab);
+        if (__any(v != 0)) coop_add_w(accw, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab, LaneField{});
     }
     if (w == 0 && valid) {
         Jac acc;
@@ -1379,6 +1447,118 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
     }
 #endif
 }
+
+#if FLM_COOP_MODJ
+// The cooperative kernel with every field element spread over a 16-lane row (flm_fe_row.h): a
+// workgroup is the same four waves (formula roles w0..w3 as coop_dbl_w / coop_add_w), each wave
+// holding four scalar multiplications, one per row.  A row multiplication is ~110 instructions per
+// lane against ~258 for the per-lane Montgomery one, so each level of the formulas is that much
+// shorter; in exchange the batch takes 16x the lanes.  For batches that leave most SIMDs idle --
+// one G = 8 rank's share of the c5 pairs (ceil(962/8) x 20 products), the agents' ECDH batches --
+// that is the trade to make (tools/ec_row_model.py).  Values stay in normal
+// form inside; the result is converted to the Montgomery Jacobian planes ec_finish_kernel reads.
+__device__ constexpr uint32_t kBn[8] = {0x27d2604bu, 0x3bce3c3eu, 0xcc53b0f6u, 0x651d06b0u,
+                                        0x769886bcu, 0xb3ebbd55u, 0xaa3a93e7u, 0x5ac635d8u};  // b
+
+__global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_kernel(const uint8_t *__restrict__ points,
+                                                                  const uint8_t *__restrict__ scalars,
+                                                                  int per_element, int T, int D,
+                                                                  uint32_t *__restrict__ jac,
+                                                                  uint32_t *__restrict__ flags) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ uint32_t S[kCoopSlots * 64];   // exchange slots, one word per lane
+    __shared__ uint32_t tab[9 * 3 * 64];      // (2t+1) P, t = 0..7, + a spare entry
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    RowField f;
+    f.K = row::make_ctx();
+    const size_t g = (size_t)blockIdx.x * 4 + (lane >> 4);
+    const bool valid = g < (size_t)T * D;
+    const int j = valid ? (int)(g / D) : 0;
+    const int i = valid ? (int)(g - (size_t)j * D) : 0;
+    // the point: lane r < 8 holds limb r of x and of y (the wire is big endian)
+    uint32_t x = 0, y = 0;
+    if (valid && r < 8) {
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(points + g * 64);
+        x = __builtin_bswap32(pw[7 - r]);
+        y = __builtin_bswap32(pw[15 - r]);
+    }
+    // x, y < p and y^2 == x^3 - 3x + b (every lane runs every row operation: no divergence around
+    // the carry loops' wave-wide votes)
+    const uint32_t rhs = f.add(f.sub(f.mul(f.sqr(x), x), f.add(f.add(x, x), x)), r < 8 ? kBn[r & 7] : 0u);
+    const bool in_x = row::row_all8(row::canon(x, f.K) == x, f.K);
+    const bool in_y = row::row_all8(row::canon(y, f.K) == y, f.K);
+    const bool on_c = row::row_all8(row::canon(f.sqr(y), f.K) == row::canon(rhs, f.K), f.K);
+    const bool ok = in_x && in_y && on_c;
+    if (w == 0 && valid && !ok && r == 0) atomicOr(&flags[i], 2u);
+    JacWT<uint32_t> PW;
+    PW.X = ok ? x : f.one();
+    PW.Y = ok ? y : f.one();
+    PW.Z = ok ? f.one() : 0u;
+    PW.W = PW.Z;  // Z^4 of Z = 1 or 0
+    int8_t dig[kNafLen];
+    if (valid) {
+        wnaf5(scalars + (per_element ? g : (size_t)j) * 32, dig);
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < kNafLen; ++k) dig[k] = 0;
+    }
+    // table of odd multiples (2k+1) P: 2P into entry 1 as the addend, then entry k = entry k-1 + 2P
+    JacWT<uint32_t> P2 = PW;
+    coop_dbl_w(P2, w, lane, S, f);
+    if (w == 0) {
+        tab[0 * 64 + lane] = PW.X;
+        tab[1 * 64 + lane] = PW.Y;
+        tab[2 * 64 + lane] = PW.Z;
+        tab[3 * 64 + lane] = P2.X;
+        tab[4 * 64 + lane] = P2.Y;
+        tab[5 * 64 + lane] = P2.Z;
+    }
+    __syncthreads();
+    JacWT<uint32_t> t = PW;
+#pragma unroll 1
+    for (int k = 1; k < 8; ++k) {
+        coop_add_w(t, true, 1, false, w, lane, S, tab, f);
+        if (w == 0) {
+            uint32_t *q = tab + (size_t)(k == 1 ? 8 : k) * 3 * 64;
+            q[lane] = t.X;
+            q[64 + lane] = t.Y;
+            q[128 + lane] = t.Z;
+        }
+        __syncthreads();
+    }
+    if (w == 0) {
+        const uint32_t *q = tab + (size_t)8 * 3 * 64;
+        tab[3 * 64 + lane] = q[lane];
+        tab[4 * 64 + lane] = q[64 + lane];
+        tab[5 * 64 + lane] = q[128 + lane];
+    }
+    __syncthreads();
+    JacWT<uint32_t> acc;
+    acc.X = acc.Y = f.one();
+    acc.Z = acc.W = 0u;
+#pragma unroll 1
+    for (int k = kNafLen - 1; k >= 0; --k) {
+        coop_dbl_w(acc, w, lane, S, f);
+        const int v = dig[k];
+        if (__any(v != 0)) coop_add_w(acc, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab, f);
+    }
+    if (w == 0) {
+        // to the Montgomery form of ec_finish_kernel (x R mod p; R mod p = kOne as a normal value),
+        // canonical; an invalid point went in as infinity (1, 1, 0) and comes out as (R, R, 0)
+        const uint32_t rm = r < 8 ? kOne[r & 7] : 0u;
+        const uint32_t X = row::canon(f.mul(acc.X, rm), f.K);
+        const uint32_t Y = row::canon(f.mul(acc.Y, rm), f.K);
+        const uint32_t Z = row::canon(f.mul(acc.Z, rm), f.K);
+        if (valid && r < 8) {
+            uint32_t *o = jac + (size_t)j * 24 * D + i;
+            o[(size_t)r * D] = X;
+            o[(size_t)(8 + r) * D] = Y;
+            o[(size_t)(16 + r) * D] = Z;
+        }
+    }
+}
+#endif  // FLM_COOP_MODJ
 
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
 // write the affine wire point and optionally SHA-256(x||y).
@@ -1560,6 +1740,14 @@ hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int 
             return hipErrorInvalidValue;
         return hipGetLastError();
     }
+#if FLM_COOP_MODJ
+    if (coop == 2) {  // one element per 16-lane row: four scalar multiplications per workgroup
+        const size_t n = (size_t)T * D;
+        hipLaunchKernelGGL(ec_mul_row_kernel, dim3((unsigned)((n + 3) / 4)), dim3(64 * kCoopWaves), 0, stream,
+                           d_points, d_scalars, per_element, T, D, d_jac, d_flags);
+        return hipGetLastError();
+    }
+#endif
     if (coop) {
         const size_t n = (size_t)T * D;
         hipLaunchKernelGGL(ec_mul_coop_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kCoopWaves), 0, stream,

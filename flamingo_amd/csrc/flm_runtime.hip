@@ -127,7 +127,8 @@ struct flm_ctx {
     int tune_ec_spread = 0;     // KiB of LDS reserved per 64-lane EC workgroup (0 = none): caps EC waves per CU
                                 // so a CU-masked dispatch spreads them one per SIMD instead of packing two
     int tune_ec_terms = 1;      // combine terms per lane (1, 2, 4: Straus, shared doublings)
-    int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 0: one
+    int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 2: four
+                                // waves per 4, each element on a 16-lane row (ec_mul_row_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
@@ -1242,7 +1243,7 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
         if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_terms must be 1, 2 or 4");
         ctx->tune_ec_terms = value;
     } else if (k == "ec_coop") {
-        if (value < -1 || value > 1) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0 or 1");
+        if (value < -1 || value > 2) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0, 1 or 2");
         ctx->tune_ec_coop = value;
     } else if (k == "ec_threads") {
         if (value != 64 && value != 128 && value != 256)

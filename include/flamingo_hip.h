@@ -166,9 +166,11 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              scalar-multiplication kernel.
  *   "ec_waves" 1 (default: uncapped registers) | 4 | 8 minimum waves per SIMD the
  *              scalar-multiplication kernel is compiled for (more waves, more spills).
- *   "ec_coop"  -1 (default: auto) | 0 | 1: scalar multiplications with four waves per 64 of
+ *   "ec_coop"  -1 (default: auto) | 0 | 1 | 2: scalar multiplications with four waves per 64 of
  *              them, the field multiplications of each point doubling and addition spread over
- *              the waves (a shorter latency chain for batches that leave most SIMDs idle).
+ *              the waves (a shorter latency chain for batches that leave most SIMDs idle); 2:
+ *              the same with every field element on a 16-lane row (four products per workgroup,
+ *              ~110 instructions per multiplication against ~258).
  *              Auto: cooperative when the batch fits one pass of the device (<= 128 products
  *              per CU), else one lane per product.
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine

@@ -17,12 +17,13 @@ import ec_oracle as E
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[(0, 1), (1, 1), (0, 2), (0, 4)],
-                ids=["per_lane", "coop", "straus2", "straus4"])
+@pytest.fixture(scope="module", params=[(0, 1), (1, 1), (2, 1), (0, 2), (0, 4)],
+                ids=["per_lane", "coop", "row", "straus2", "straus4"])
 def eng(request):
     """Every test runs with each scalar-multiplication kernel: one lane per product (ec_mul_kernel),
-    four cooperating waves per 64 products (ec_mul_coop_kernel), and 2 / 4 combine terms per lane
-    sharing one chain of doublings (ec_mul_straus_kernel; the combine only)."""
+    four cooperating waves per 64 products (ec_mul_coop_kernel), the same with every field element
+    on a 16-lane row (ec_mul_row_kernel, flm_fe_row.h), and 2 / 4 combine terms per lane sharing one
+    chain of doublings (ec_mul_straus_kernel; the combine only)."""
     from flamingo_amd import MaskEngine
     e = MaskEngine(0)
     e.set_tuning("ec_coop", request.param[0])
