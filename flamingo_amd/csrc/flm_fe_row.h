@@ -12,12 +12,13 @@
 //   * the columns (96 bits each) become 16 saturated limbs by carry passes along the row;
 //   * NIST's fast reduction for p = 2^256 - 2^224 + 2^192 + 2^96 - 1: limb r of the result is
 //     c_r + sum_k A[r][k] c_(8+k), A a fixed 8x8 matrix of -1..3 (each c_(8+k) broadcast once, two
-//     multiply-adds per k with the lane's own coefficients);
+//     multiply-adds per k: the lane's own coefficient A + 1 >= 0, and the row-uniform sum it biases);
 //   * signed carry passes along the row, the carry out of limb 7 folded back as
 //     t 2^256 = t (2^224 - 2^192 - 2^96 + 1) (mod p), until no limb carries.
 // Values are kept lazily in [0, 2^256) (possibly >= p); canon() gives the representative < p.
-// The carry passes loop until no lane of the wave carries (wave-uniform branch): one pass for
-// almost every input, up to ~10 for adversarial ones (tools/ec_row_model.py runs the same loops).
+// The carry passes loop until no lane of the wave carries (wave-uniform branch after each pass): one
+// pass for almost every input, up to ~10 for adversarial ones (tools/ec_row_model.py runs the same
+// loops).
 // Normal form (no Montgomery factor): the reduction is the parallel NIST fold, not the sequential
 // Montgomery digit chain.
 #pragma once
@@ -49,12 +50,12 @@ __device__ constexpr uint32_t kPl[8] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0
 
 // Per-lane constants, built once per kernel (kept in VGPRs).
 struct Ctx {
-    uint32_t apos[8];  // max(A[r][k], 0) for r < 8, else 0
-    uint32_t aneg[8];  // 1 where A[r][k] == -1, else 0
+    uint32_t a1[8];    // A[r][k] + 1 (0..4) for r < 8, else 0: the fold adds sum_k a1 c_(8+k) - sum_k c_(8+k)
+    uint32_t one8;     // 1 for r < 8, else 0 (the weight of that row-uniform sum)
     int32_t fco;       // the top carry's weight at limb r: +1 (r = 0, 7), -1 (r = 3, 6), else 0
     uint32_t lo8;      // ~0 for r < 8, else 0
     uint32_t plimb;    // limb r of p (0 for r >= 8)
-    uint32_t rbit;     // 1 << (lane & ~15): this row's first lane in a wave-wide ballot
+    uint32_t rbit;     // lane & ~15: this row's first bit in a wave-wide ballot
 };
 
 __device__ __forceinline__ Ctx make_ctx() {
@@ -62,11 +63,8 @@ __device__ __forceinline__ Ctx make_ctx() {
     const int lane = (int)(threadIdx.x & 63), r = lane & 15;
     const bool low = r < 8;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int a = low ? kFold[r & 7][k] : 0;
-        c.apos[k] = a > 0 ? (uint32_t)a : 0u;
-        c.aneg[k] = a < 0 ? 1u : 0u;
-    }
+    for (int k = 0; k < 8; ++k) c.a1[k] = low ? (uint32_t)(kFold[r & 7][k] + 1) : 0u;
+    c.one8 = low ? 1u : 0u;
     c.fco = !low ? 0 : (r == 0 || r == 7) ? 1 : (r == 3 || r == 6) ? -1 : 0;
     c.lo8 = low ? ~0u : 0u;
     c.plimb = low ? kPl[r] : 0u;
@@ -76,18 +74,20 @@ __device__ __forceinline__ Ctx make_ctx() {
 
 // Signed carry passes: v (lanes r < 8: a signed 64-bit limb value, lanes >= 8: 0) -> the limbs of a
 // value congruent mod p in [0, 2^256).  The carry out of limb r moves to limb r + 1; limb 7's is
-// folded back at limbs 0, 3, 6, 7.
+// folded back at limbs 0, 3, 6, 7.  Every caller's input carries somewhere (a product fold, a
+// limb-wise add or subtract), so the first pass runs unconditionally and the wave-wide vote comes
+// after it: one branch for almost every input.
 __device__ __forceinline__ uint32_t snorm(int64_t v, const Ctx &K) {
     int32_t c = (int32_t)(v >> 32);
     uint32_t lo = (uint32_t)v;
 #pragma unroll 1
-    while (__any(c != 0)) {
+    do {
         const int32_t t = (int32_t)bcast<7>((uint32_t)c);
         const int32_t cin = (int32_t)(shr<1>((uint32_t)c) & K.lo8);
         v = (int64_t)(uint64_t)lo + (int64_t)(cin + t * K.fco);
         c = (int32_t)(v >> 32);
         lo = (uint32_t)v;
-    }
+    } while (__any(c != 0));
     return lo;
 }
 
@@ -119,23 +119,24 @@ __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b, const Ctx &K) {
     uint64_t s = (uint64_t)(uint32_t)acc + shr<1>((uint32_t)(acc >> 32)) + shr<2>(hi);
     uint32_t c = (uint32_t)(s >> 32), lo = (uint32_t)s;
 #pragma unroll 1
-    while (__any(c != 0)) {
+    do {  // the three-term sums carry in some lane of every product: first pass unconditional
         s = (uint64_t)lo + shr<1>(c);
         c = (uint32_t)(s >> 32);
         lo = (uint32_t)s;
-    }
-    // NIST fold: limb r = c_r + sum_k A[r][k] c_(8+k) (lanes >= 8 start from 0)
-    uint64_t pos = (uint64_t)(lo & K.lo8), neg = 0;
+    } while (__any(c != 0));
+    // NIST fold: limb r = c_r + sum_k A[r][k] c_(8+k) = c_r + sum_k (A[r][k] + 1) c_(8+k) - sum_k c_(8+k),
+    // the coefficients made non-negative so every term is one v_mad_u64_u32 (lanes >= 8 stay 0)
+    uint64_t pos = (uint64_t)(lo & K.lo8), hsum = 0;
 #define FLM_ROW_FOLD(k)                               \
     {                                                 \
         const uint32_t h = bcast<8 + k>(lo);          \
-        pos += (uint64_t)h * K.apos[k];               \
-        neg += (uint64_t)h * K.aneg[k];               \
+        pos += (uint64_t)h * K.a1[k];                 \
+        hsum += (uint64_t)h * K.one8;                 \
     }
     FLM_ROW_FOLD(0) FLM_ROW_FOLD(1) FLM_ROW_FOLD(2) FLM_ROW_FOLD(3)
     FLM_ROW_FOLD(4) FLM_ROW_FOLD(5) FLM_ROW_FOLD(6) FLM_ROW_FOLD(7)
 #undef FLM_ROW_FOLD
-    return snorm((int64_t)(pos - neg), K);
+    return snorm((int64_t)(pos - hsum), K);
 }
 
 __device__ __forceinline__ uint32_t sqr(uint32_t a, const Ctx &K) { return mul(a, a, K); }
@@ -169,12 +170,12 @@ __device__ __forceinline__ uint32_t canon(uint32_t a, const Ctx &K) {
     int32_t c = (int32_t)(d >> 32), top = 0;
     uint32_t lo = (uint32_t)d;
 #pragma unroll 1
-    while (__any(c != 0)) {
+    do {
         top += (int32_t)bcast<7>((uint32_t)c);
         d = (int64_t)(uint64_t)lo + (int32_t)(shr<1>((uint32_t)c) & K.lo8);
         c = (int32_t)(d >> 32);
         lo = (uint32_t)d;
-    }
+    } while (__any(c != 0));
     return top == 0 ? lo : a;
 }
 

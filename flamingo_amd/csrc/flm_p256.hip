@@ -1390,10 +1390,14 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
         accw.X = inf.X; accw.Y = inf.Y; accw.Z = inf.Z;
         accw.W = inf.Z;  // 0
     }
+    // the next digit is read from scratch before the doubling, so its latency hides under it (read
+    // after the doubling, every step waited for the scratch load: tools/probes/ec_row_split.py)
+    int v_next = dig[kNafLen - 1];
 #pragma unroll 1
     for (int k = kNafLen - 1; k >= 0; --k) {
+        const int v = v_next;
+        if (k > 0) v_next = dig[k - 1];
         coop_dbl_w(accw, w, lane, S, LaneField{});
-        const int v = dig[k];
         if (__any(v != 0)) coop_add_w(accw, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab, LaneField{});
     }
     if (w == 0 && valid) {
@@ -1537,10 +1541,12 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_kernel(const uint8
     JacWT<uint32_t> acc;
     acc.X = acc.Y = f.one();
     acc.Z = acc.W = 0u;
+    int v_next = dig[kNafLen - 1];  // read one step ahead, as ec_mul_coop_kernel
 #pragma unroll 1
     for (int k = kNafLen - 1; k >= 0; --k) {
+        const int v = v_next;
+        if (k > 0) v_next = dig[k - 1];
         coop_dbl_w(acc, w, lane, S, f);
-        const int v = dig[k];
         if (__any(v != 0)) coop_add_w(acc, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab, f);
     }
     if (w == 0) {

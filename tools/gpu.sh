@@ -11,7 +11,10 @@
 #                the sharded c4 and c5 paths end to end, correctness only)
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
 #   rccl         tools/rccl_clique_smoke.py (forced one-device RCCL clique + world-1 forced collectives),
-#                then the same under rocprofv3 --kernel-trace --memory-copy-trace --stats
+#                then the same with AMD_LOG_LEVEL=4: the kernels it dispatched (RCCL's included)
+#   rccltrace    the same script under rocprofv3 --kernel-trace --stats (put it last in a call)
+#   ecpmc:K      rocprofv3 PMC pass (VALU/SALU instructions, wave cycles, waits) of the combine at D = 4
+#                with ec_coop K (1: per-lane field, 2: row field)
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
 #   py:SCRIPT[:ARG]  python tools/SCRIPT [ARG] (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
@@ -56,9 +59,23 @@ for step in "$@"; do
       timeout -k 10 300 python -u tools/rccl_clique_smoke.py > "$O/${TAG}_rccl_clique.log" 2>&1 \
         || { tail -30 "$O/${TAG}_rccl_clique.log"; exit 1; }
       tail -2 "$O/${TAG}_rccl_clique.log"
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
-        -d "$O/${TAG}_rccl_trace" -o run -- python3 "$R/tools/rccl_clique_smoke.py" > "$O/${TAG}_rccl_trace.log" 2>&1) \
+      # the HIP runtime's own launch log names every kernel dispatched (RCCL's included)
+      AMD_LOG_LEVEL=4 timeout -k 10 300 python -u tools/rccl_clique_smoke.py gloo > "$O/${TAG}_rccl_amdlog.out" \
+        2> "$O/${TAG}_rccl_amdlog.err" || { tail -20 "$O/${TAG}_rccl_amdlog.out"; exit 1; }
+      python tools/kernel_log_summary.py "$O/${TAG}_rccl_amdlog.err" "$O/${TAG}_rccl_kernels.json" && rm -f "$O/${TAG}_rccl_amdlog.err" ;;
+    rccltrace)
+      # rocprofv3 kernel trace of the same script (last step of a call: with RCCL loaded the
+      # profiled process has crashed in its exit-time destructors, after every check passed)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$O/${TAG}_rccl_trace" -o run -- python3 "$R/tools/rccl_clique_smoke.py" gloo > "$O/${TAG}_rccl_trace.log" 2>&1) \
         || { tail -20 "$O/${TAG}_rccl_trace.log"; exit 1; } ;;
+    ecpmc:*)
+      # one PMC pass over tools/ec_bench.py (the combine, T = 20, Lagrange scalars) with ec_coop ${step#ecpmc:}
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \
+        SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_INSTS_SALU --output-format csv \
+        -d "$O/${TAG}_ecpmc${step#ecpmc:}" -o run -- python3 "$R/tools/ec_bench.py" --D 4 --T 20 --reps 3 \
+        --scalars lagrange --coop "${step#ecpmc:}" > "$O/${TAG}_ecpmc${step#ecpmc:}.log" 2>&1) \
+        || { tail -20 "$O/${TAG}_ecpmc${step#ecpmc:}.log"; exit 1; } ;;
     prof)
       bash tools/gpu_prof.sh "$TAG" || exit 1 ;;
     clock)

@@ -7,7 +7,11 @@ under rocprofv3 is the evidence that they execute; tools/gpu.sh step `rccl`).
 * the library communicator of one process per GPU (init_rccl -> flm_comm_init_rank) at world 1
   with force_collective: ShardedRound's flm_reduce_scatter_dev (synchronous and pipelined) and
   ShardedReconstruction's flm_all_gather_dev + flm_reduce_scatter_dev.
-Every result is checked against the C oracle or the |U| invariant; exits non-zero on a mismatch."""
+Every result is checked against the C oracle or the |U| invariant; exits non-zero on a mismatch.
+Argument: the torch.distributed backend of the world-1 group (nccl, default, or gloo).  The
+collectives under test are the library's own RCCL communicator either way; gloo keeps torch's
+ProcessGroupNCCL out of the process, which the rocprofv3 trace of this script needs (under the
+profiler that process group's teardown crashed at exit, after every check had passed)."""
 import os
 import sys
 
@@ -78,7 +82,11 @@ grp.close()
 # ---- one process per GPU at world 1, forced through the collectives
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29573")
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+backend = sys.argv[1] if len(sys.argv) > 1 else "nccl"
+if backend == "nccl":
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+else:
+    dist.init_process_group("gloo", rank=0, world_size=1)
 eng = MaskEngine(0)
 init_rccl(eng)
 check("library communicator attached", eng.has_comm() and eng.comm_size() == (1, 0))
