@@ -1283,14 +1283,19 @@ static int ec_dims(flm_ctx *ctx, int T, int D) {
     return 0;
 }
 
-// Cooperative scalar multiplication (four waves, 78 KiB of LDS per 64 products: two workgroups per CU)
-// when the whole batch fits one pass of the device -- the latency-bound case, e.g. c5 seed recovery
-// (19,240 products) or one rank's pair chunk; bigger batches, and launches the caller confines to a
-// few CUs (ServerReconstruction's CU-split stream sets 0), keep one lane per product.
+// Cooperative scalar multiplication when the whole batch fits one pass of the device -- the
+// latency-bound case: the row-field kernel (four waves per 4 products, ec_mul_row_kernel) up to
+// 20 products per CU, e.g. one G = 8 rank's pair chunk (ceil(962/8) x 20 = 2,420: 0.77 against
+// 1.20 ms per-lane-field cooperative, tools/probes/ec_kernel_sweep.py, profiles/r04_ec_kernel_sweep.log;
+// still 13 % ahead at 4,800, 39 % behind at 9,620), then the per-lane-field cooperative kernel (four
+// waves per 64 products, 78 KiB of LDS: two workgroups per CU) up to 128 per CU, e.g. the whole c5
+// seed recovery (19,240 products); bigger batches, and launches the caller confines to a few CUs
+// (ServerReconstruction's CU-split stream sets 0), keep one lane per product.
 int ec_coop(flm_ctx *ctx, size_t n) {
     if (ctx->tune_ec_coop >= 0) return ctx->tune_ec_coop;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
+    if (n <= (size_t)cus * 20) return 2;
     return n <= (size_t)cus * 2 * 64 ? 1 : 0;
 }
 

@@ -59,7 +59,8 @@ class ServerReconstruction:
             raise ValueError("ec_terms must be 1, 2 or 4")
         self.ec_terms = int(ec_terms)
         self.ec_spread = int(ec_spread)   # KiB of LDS per EC workgroup on the confined CUs (flm_set_tuning ec_spread)
-        self.ec_coop = int(ec_coop)       # on the confined CUs: 0 one lane per product, 1 four cooperating waves
+        self.ec_coop = int(ec_coop)       # on the confined CUs: 0 one lane per product, 1 four cooperating waves,
+                                          # 2 the same with the row field (flm_fe_row.h)
         self.pass1_min_items = pass1_min_items
         if not 0.0 <= pair_split < 1.0:
             raise ValueError("pair_split must be in [0, 1)")

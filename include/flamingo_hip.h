@@ -171,8 +171,8 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              the waves (a shorter latency chain for batches that leave most SIMDs idle); 2:
  *              the same with every field element on a 16-lane row (four products per workgroup,
  *              ~110 instructions per multiplication against ~258).
- *              Auto: cooperative when the batch fits one pass of the device (<= 128 products
- *              per CU), else one lane per product.
+ *              Auto: the row kernel up to 20 products per CU, the cooperative kernel up to 128
+ *              per CU (one pass of the device), else one lane per product.
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
  *              (Straus: the terms share one chain of doublings); ignored when the combine
  *              runs cooperatively.

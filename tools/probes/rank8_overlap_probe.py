@@ -55,6 +55,13 @@ if "--coop-fine" in sys.argv:   # around the best of --coop-only, two passes
     cases = cases[:2] + [(f"cu_split_coop_{c}_items{mi}",
                            dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=mi), True)
                           for c in (56, 64, 72, 80, 96) for mi in (2048, 4096)] * 2
+if "--row" in sys.argv:   # round 4: the row-field cooperative kernel (ec_coop 2), unpartitioned and on its own CUs
+    cases = cases[:2] + [(f"cu_split_row_{c}_items4096",
+                          dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=2, pass1_min_items=4096), True)
+                         for c in (64, 96, 128, 160)] + [
+                        (f"cu_split_coop_{c}_items4096",
+                         dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=4096), True)
+                        for c in (72, 96)]
 for name, kw, ovl in cases:
     rec = ServerReconstruction(eng, **kw)
     dst = ref if name == "sequential" else out
