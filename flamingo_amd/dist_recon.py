@@ -62,7 +62,7 @@ class ShardedReconstruction:
     so a one-GPU box executes the exact code the G-GPU run takes."""
 
     def __init__(self, engine, L: int, group=None, device=None, comm: str | None = None, ec_cus: int = 0,
-                 cu_pick: str = "first", force_collective: bool = False):
+                 cu_pick: str = "first", force_collective: bool = False, ec_coop: int = 1):
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -80,6 +80,12 @@ class ShardedReconstruction:
                               and engine.comm_size() == (self.world, self.rank)) else "torch"
         self.comm = comm
         self.ec_cus = int(ec_cus)
+        # the scalar-multiplication kernel on the confined CUs (flm_set_tuning ec_coop; unconfined, the
+        # library's auto choice stands): the per-lane-field cooperative kernel, 1.45 ms for one G = 8
+        # rank's shares -> final on 72 CUs against 1.83 / 1.53 ms for the row-field kernel on 64 / 128
+        # (its 16x more waves crowd a confined set; tools/probes/rank8_overlap_probe.py --row,
+        # profiles/r04_rank8_row.log)
+        self.ec_coop = int(ec_coop)
         self.pass_stream = None
         if self.ec_cus > 0:
             from .reconstruct import pick_cus
@@ -101,6 +107,16 @@ class ShardedReconstruction:
                 b.fill_(fill)
             self._bufs[name] = b
         return b
+
+    def _ec_combine(self, c1, shares, lambdas, seeds, flags):
+        """The rank's pair chunk on the side stream; on confined CUs with the ec_coop kernel."""
+        if self.ec_cus > 0:
+            self.eng.set_tuning("ec_coop", self.ec_coop)
+        try:
+            self.eng.ec_combine_dev(c1, shares, lambdas, seeds, flags, stream=self.side)
+        finally:
+            if self.ec_cus > 0:
+                self.eng.set_tuning("ec_coop", -1)
 
     def _pass_begin(self, ready, main):
         """The stream Shamir and the self-mask pass run on: the caller's, or (ec_cus > 0) the
@@ -168,7 +184,7 @@ class ShardedReconstruction:
         ready.record(main)
         if Dr:
             self.side.wait_event(ready)
-            eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
+            self._ec_combine(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags)
         done = torch.cuda.Event()
         done.record(self.side)
         ps = self._pass_begin(ready, main)
@@ -224,7 +240,7 @@ class ShardedReconstruction:
         ready.record(main)
         if Dr:
             self.side.wait_event(ready)
-            eng.ec_combine_dev(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags, stream=self.side)
+            self._ec_combine(c1_mine, pair_shares_mine, lambdas, chunk[:Dr], flags)
         done = torch.cuda.Event()
         done.record(self.side)
         ps = self._pass_begin(ready, main)
