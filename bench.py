@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL; the real multi-GPU path) or gloo (test only: ranks sharing one GPU)")
     ap.add_argument("--no-group", action="store_true", help="skip the single-process device-group leg")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live HBM-traffic passes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over "
+                         "bench.py --profile as child processes); the committed profile's figure is reported")
     ap.add_argument("--group-leg", action="store_true",
                     help="internal: run only the device-group leg and print its JSON (bench.py runs it as a child "
                          "process under a time limit, so a clique that cannot come up cannot hang the bench)")
@@ -494,6 +497,13 @@ def main():
             res["with_copy"] = with_copy(eng, torch, rows_on, sseeds, ssigns, L, len(online))
         if not args.no_cpu:
             res["cpu_baseline"] = cpu_baseline(rows_on, sseeds, ssigns, L, out)
+        if not args.no_pmc:
+            live = live_traffic(args, rows_rank, L, int(K))
+            res["roofline"]["traffic_live"] = live
+            if "bytes" in live:
+                res["roofline"]["traffic_committed"] = res["roofline"].get("traffic")
+                res["roofline"]["traffic"] = live["bytes"]
+                res["roofline"]["traffic_source"] = live["source"]
     if G > 1 and not args.profile and not args.no_copy:
         res["with_copy"] = with_copy_sharded(torch, dist, rnd, rows_on, d_seeds, d_signs, stream, len(online), L,
                                              coll_dev)
@@ -1133,6 +1143,55 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
                         "shard; reduce-scatter ("
                         + ("library RCCL communicator, ncclUint32" if rec.comm == "rccl" else f"torch.distributed {backend}")
                         + ")"}
+
+
+def live_traffic(args, rows, L, K, timeout=180):
+    """HBM bytes per launch of the dominant kernel, measured in this run on this box: two rocprofv3
+    PMC passes over `bench.py --profile` (the same c4 workload), run as child processes of this one
+    (never an exec), one counter group each -- FETCH_SIZE takes 3 of the 4 TCC counters and
+    WRITE_SIZE 2 (MI355X_MICROARCH.md) -- with gfx950's correction: FETCH_SIZE reports half the bytes
+    of a wide coalesced stream, so read bytes = 2 x FETCH_SIZE KiB; WRITE_SIZE is exact for 16-B
+    stores.  Averaged over the child's items_kernel<1> dispatches.  A pass that fails or exceeds
+    `timeout` s (killed) gives {"error": ...}; the committed profile's figure then stays."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if not rp:
+        return {"error": "rocprofv3 not found"}
+    child = [sys.executable, os.path.abspath(__file__), "--profile", "--steps", "10", "--warmup", "2",
+             "--settle-ms", "50", "--total-clients", str(args.total_clients), "--log2-L", str(args.log2_L),
+             "--dropout", str(args.dropout)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    kib = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, ctr)
+            try:
+                r = subprocess.run([rp, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--", *child],
+                                   capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+            except subprocess.TimeoutExpired:
+                return {"error": f"rocprofv3 --pmc {ctr} did not finish in {timeout} s (killed)"}
+            if r.returncode != 0:
+                return {"error": f"rocprofv3 --pmc {ctr} exited {r.returncode}: {r.stderr.strip()[-300:]}"}
+            per = {}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    if "items_kernel<1" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                        per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+            if not per:
+                return {"error": f"no items_kernel<1 dispatch in the {ctr} pass"}
+            kib[ctr] = (sum(per.values()) / len(per), len(per))
+    read = 2.0 * kib["FETCH_SIZE"][0] * 1024
+    write = kib["WRITE_SIZE"][0] * 1024
+    alg = 4.0 * rows * L + 4.0 * L
+    return {"bytes": int(read + write), "read_bytes_corrected": int(read), "write_bytes": int(write),
+            "algorithmic_bytes": int(alg), "traffic_over_algorithmic": round((read + write) / alg, 4),
+            "dispatches": {"FETCH_SIZE": kib["FETCH_SIZE"][1], "WRITE_SIZE": kib["WRITE_SIZE"][1]},
+            "source": "this run: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, over bench.py --profile (same workload, "
+                      "this box), FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per items_kernel<1> launch"}
 
 
 def committed_cpi():
