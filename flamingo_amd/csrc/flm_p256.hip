@@ -1455,7 +1455,7 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
 #if FLM_COOP_MODJ
 // The cooperative kernel with every field element spread over a 16-lane row (flm_fe_row.h): a
 // workgroup is the same four waves (formula roles w0..w3 as coop_dbl_w / coop_add_w), each wave
-// holding four scalar multiplications, one per row.  A row multiplication is ~110 instructions per
+// holding four scalar multiplications, one per row.  A row multiplication is ~93 instructions per
 // lane against ~258 for the per-lane Montgomery one, so each level of the formulas is that much
 // shorter; in exchange the batch takes 16x the lanes.  For batches that leave most SIMDs idle --
 // one G = 8 rank's share of the c5 pairs (ceil(962/8) x 20 products), the agents' ECDH batches --
