@@ -1145,6 +1145,22 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
                         + ")"}
 
 
+def pmc_per_dispatch(d, ctr, kernel="items_kernel<1,"):
+    """rocprofv3 --pmc CSV output under directory d: counter `ctr` per dispatch of `kernel`, summed
+    over the CSV's per-instance rows (one row per XCD / block instance).  The default names the
+    template argument with its comma: `items_kernel<1` alone also matches `items_kernel<16, ...>`
+    (the one launch that makes the bench's rows), whose 4 GiB of writes then pollute the average."""
+    import csv
+    import glob
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == ctr:
+                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    return per
+
+
 def live_traffic(args, rows, L, K, timeout=180):
     """HBM bytes per launch of the dominant kernel, measured in this run on this box: two rocprofv3
     PMC passes over `bench.py --profile` (the same c4 workload), run as child processes of this one
@@ -1153,8 +1169,6 @@ def live_traffic(args, rows, L, K, timeout=180):
     of a wide coalesced stream, so read bytes = 2 x FETCH_SIZE KiB; WRITE_SIZE is exact for 16-B
     stores.  Averaged over the child's items_kernel<1> dispatches.  A pass that fails or exceeds
     `timeout` s (killed) gives {"error": ...}; the committed profile's figure then stays."""
-    import csv
-    import glob
     import shutil
     import subprocess
     import tempfile
@@ -1176,11 +1190,7 @@ def live_traffic(args, rows, L, K, timeout=180):
                 return {"error": f"rocprofv3 --pmc {ctr} did not finish in {timeout} s (killed)"}
             if r.returncode != 0:
                 return {"error": f"rocprofv3 --pmc {ctr} exited {r.returncode}: {r.stderr.strip()[-300:]}"}
-            per = {}
-            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                for row in csv.DictReader(open(f)):
-                    if "items_kernel<1" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
-                        per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+            per = pmc_per_dispatch(d, ctr)
             if not per:
                 return {"error": f"no items_kernel<1 dispatch in the {ctr} pass"}
             kib[ctr] = (sum(per.values()) / len(per), len(per))
@@ -1224,7 +1234,7 @@ def committed_traffic(rows, L, K):
         if (wl.get("rows"), wl.get("L"), wl.get("K")) != (rows, L, K):
             continue
         for k, v in d.get("counters", {}).items():
-            if k.startswith("flm::items_kernel<1") and "hbm_traffic_bytes" in v:
+            if k.startswith("flm::items_kernel<1,") and "hbm_traffic_bytes" in v:
                 best = {"bytes": int(v["hbm_traffic_bytes"]), "source": os.path.relpath(f, ROOT)}
     return best
 

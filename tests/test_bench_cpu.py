@@ -74,3 +74,22 @@ def test_group_leg_failure_becomes_an_error_field():
     args = argparse.Namespace(total_clients=64, log2_L=12, dropout=0.0, group_devices="", no_copy=True)
     res = bench.group_leg_subprocess(args, timeout=240)
     assert set(res) == {"error"} and "exited" in res["error"]
+
+
+def test_pmc_csv_sums_instances_per_dispatch(tmp_path):
+    """live_traffic's parser: rocprofv3 --pmc writes one CSV row per counter instance; the bytes of
+    one dispatch are their sum, other kernels and counters are ignored."""
+    d = tmp_path / "pass" / "host"
+    d.mkdir(parents=True)
+    hdr = "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
+    rows = [(1, "void flm::items_kernel<1, true>(...)", "FETCH_SIZE", 100.0),
+            (1, "void flm::items_kernel<1, true>(...)", "FETCH_SIZE", 50.5),
+            (2, "void flm::items_kernel<1, true>(...)", "FETCH_SIZE", 120.0),
+            (3, "void flm::items_kernel<16, true>(...)", "FETCH_SIZE", 999.0),
+            (2, "void flm::items_kernel<1, true>(...)", "WRITE_SIZE", 7.0)]
+    (d / "run_counter_collection.csv").write_text(
+        hdr + "".join(f'{a},"{b}",{c},{v}\n' for a, b, c, v in rows))
+    per = bench.pmc_per_dispatch(str(tmp_path / "pass"), "FETCH_SIZE")
+    assert per == {"1": 150.5, "2": 120.0}
+    assert bench.pmc_per_dispatch(str(tmp_path / "pass"), "WRITE_SIZE") == {"2": 7.0}
+    assert bench.pmc_per_dispatch(str(tmp_path / "none"), "FETCH_SIZE") == {}
