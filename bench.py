@@ -45,6 +45,9 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 G
 PROBE_CHACHA_CEILING_GWORDS = 733.0
 CPI_SUMMARY = "profiles/r02_clock_cpi_summary.json"
 CHACHA_MIX_CPI = 8.0 / 3.0       # cycles per VALU instruction of the add/xor/rotate mix at 2/2/4 cycles
+# torchrun's per-rank environment: removed for the PMC child of a rank, so it runs as world 1
+TORCHRUN_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
 CHACHA_OPS_PER_WORD = 61.5       # VALU instructions per mask word in items_kernel (PMC: 1.031e9 wave-instructions x 64 / 2^30 words, profiles/r02_profile_summary.json)
 
 
@@ -74,6 +77,11 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live HBM-traffic passes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over "
                          "bench.py --profile as child processes); the committed profile's figure is reported")
+    ap.add_argument("--profile-rank", type=int, default=0,
+                    help="internal, with --profile --profile-world G: run rank R's kernel of a G-rank round alone "
+                         "on this GPU (its clients' rows, its slot shard's masks, no collective) for the PMC passes "
+                         "of a G > 1 line")
+    ap.add_argument("--profile-world", type=int, default=1, help="internal: see --profile-rank")
     ap.add_argument("--group-leg", action="store_true",
                     help="internal: run only the device-group leg and print its JSON (bench.py runs it as a child "
                          "process under a time limit, so a clique that cannot come up cannot hang the bench)")
@@ -273,14 +281,17 @@ def main():
             print(f"warning: library RCCL communicator unavailable ({err}); using torch.distributed", file=sys.stderr)
     L = 1 << args.log2_L
     strong = not args.weak
-    N = args.total_clients if strong else args.clients_per_gpu * G
-    Ng = N // G if strong else args.clients_per_gpu
+    # --profile --profile-world G: rank R of a G-rank round, alone on this GPU (live_traffic's child)
+    Gg, Rg = (args.profile_world, args.profile_rank) if (args.profile and args.profile_world > 1 and G == 1) \
+        else (G, rank)
+    N = args.total_clients if strong else args.clients_per_gpu * Gg
+    Ng = N // Gg if strong else args.clients_per_gpu
     cfg = f"c4-n{N}-L{L}"
 
     # ---- inputs: valid masked rows, built on this GPU by the client-side kernel
     m = np.frombuffer(b"".join(P.bench_seed(cfg, i) for i in range(N)), np.uint8).reshape(N, 32)
     nbrs = P.neighbor_graph(b"\x00" * 32, 1, N, 1, encrypt=eng.chacha20_encrypt)
-    c0, c1 = client_bounds(N, G, rank)
+    c0, c1 = client_bounds(N, Gg, Rg)
     seg, d_cseeds, csigns = client_table(torch, P, m, nbrs, c0, c1, dev)
 
     g = np.random.Generator(np.random.PCG64(12345))
@@ -299,6 +310,9 @@ def main():
     torch.cuda.set_stream(stream)
     # two partial buffers: round k's reduce-scatter (RCCL, async) runs under round k+1's kernel
     rnd = ShardedRound(eng, L, buffers=2 if G > 1 else 1, comm=comm)
+    if Gg != G:  # the emulated rank's slot shard (its kernel's mask window; no exchange follows)
+        from flamingo_amd.distributed import shard_bounds
+        rnd.lo, rnd.hi = shard_bounds(L, Gg, Rg)
 
     # the rows are built last, right before the warm-up: the host-side preparation above leaves
     # the GPU idle, and MI355X ramps its clock back up over ~30 ms of load
@@ -360,7 +374,8 @@ def main():
     # ---- correctness of the timed round: out == |U| in every slot of my shard
     out = rnd.result()
     torch.cuda.synchronize()
-    ok = bool(torch.all(out == len(online)).item())
+    # (an emulated rank's partial holds only its clients' rows: no |U| to check)
+    ok = bool(torch.all(out == len(online)).item()) if Gg == G else True
     okt = torch.tensor([1 if ok else 0], device=coll_dev)
     if G > 1:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
@@ -504,6 +519,15 @@ def main():
                 res["roofline"]["traffic_committed"] = res["roofline"].get("traffic")
                 res["roofline"]["traffic"] = live["bytes"]
                 res["roofline"]["traffic_source"] = live["source"]
+    if G > 1 and not args.profile and not args.no_pmc:
+        # the same-run HBM traffic of rank 0's kernel (its PMC child runs while the other ranks wait)
+        if rank == 0:
+            live = live_traffic(args, rows_rank, L, int(K), rank=0, world=G)
+            res["roofline"]["traffic_live"] = live
+            if "bytes" in live:
+                res["roofline"]["traffic"] = live["bytes"]
+                res["roofline"]["traffic_source"] = live["source"]
+        dist.barrier()
     if G > 1 and not args.profile and not args.no_copy:
         res["with_copy"] = with_copy_sharded(torch, dist, rnd, rows_on, d_seeds, d_signs, stream, len(online), L,
                                              coll_dev)
@@ -1145,30 +1169,50 @@ def measure_c5_sharded(eng, torch, dist, P, G, rank, backend="nccl", rounds=10, 
                         + ")"}
 
 
-def pmc_per_dispatch(d, ctr, kernel="items_kernel<1,"):
-    """rocprofv3 --pmc CSV output under directory d: counter `ctr` per dispatch of `kernel`, summed
-    over the CSV's per-instance rows (one row per XCD / block instance).  The default names the
-    template argument with its comma: `items_kernel<1` alone also matches `items_kernel<16, ...>`
-    (the one launch that makes the bench's rows), whose 4 GiB of writes then pollute the average."""
+def pmc_per_dispatch(d, ctr, kernel=None):
+    """rocprofv3 --pmc CSV output under directory d: counter `ctr` per dispatch, summed over the CSV's
+    per-instance rows (one row per XCD / block instance), for one kernel: the one whose name contains
+    `kernel`, or (None) the `items_kernel` instance with the most dispatches -- the timed round's
+    kernel, whatever its template arguments (a G > 1 rank's shard kernel may differ from c4's); the
+    bench's one-off launches, such as the `items_kernel<16, ...>` that makes the rows, are single
+    dispatches.  (A name prefix is not enough: `items_kernel<1` also matches `items_kernel<16`.)
+    Returns (kernel name, {dispatch id: value}); (None, {}) when nothing matches."""
     import csv
     import glob
-    per = {}
+    by_kernel = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kernel in row["Kernel_Name"] and row["Counter_Name"] == ctr:
-                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-    return per
+                name = row["Kernel_Name"]
+                if row["Counter_Name"] != ctr or (kernel not in name if kernel else "items_kernel<" not in name):
+                    continue
+                per = by_kernel.setdefault(name, {})
+                per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    if not by_kernel:
+        return None, {}
+    name = max(by_kernel, key=lambda k: len(by_kernel[k]))
+    return name, by_kernel[name]
 
 
-def live_traffic(args, rows, L, K, timeout=180):
+def child_env(environ):
+    """The environment of a profiling child: this process's without torchrun's per-rank variables
+    (the child must run as world 1, not join the ranks' group), TMPDIR=/tmp for rocprofv3."""
+    env = {k: v for k, v in environ.items() if k not in TORCHRUN_ENV and not k.startswith("TORCHELASTIC_")}
+    env["TMPDIR"] = "/tmp"
+    return env
+
+
+def live_traffic(args, rows, L, K, timeout=180, rank=0, world=1):
     """HBM bytes per launch of the dominant kernel, measured in this run on this box: two rocprofv3
-    PMC passes over `bench.py --profile` (the same c4 workload), run as child processes of this one
+    PMC passes over `bench.py --profile` (the same workload), run as child processes of this one
     (never an exec), one counter group each -- FETCH_SIZE takes 3 of the 4 TCC counters and
     WRITE_SIZE 2 (MI355X_MICROARCH.md) -- with gfx950's correction: FETCH_SIZE reports half the bytes
     of a wide coalesced stream, so read bytes = 2 x FETCH_SIZE KiB; WRITE_SIZE is exact for 16-B
-    stores.  Averaged over the child's items_kernel<1> dispatches.  A pass that fails or exceeds
-    `timeout` s (killed) gives {"error": ...}; the committed profile's figure then stays."""
+    stores.  Averaged over the child's dispatches of the round's kernel (pmc_per_dispatch).
+    world > 1: the child runs rank `rank`'s kernel of a `world`-rank round alone on this GPU
+    (--profile-rank / --profile-world: its clients' rows over all L slots, its shard's masks, no
+    collective), with torchrun's environment removed so it does not join the running ranks' group.
+    A pass that fails or exceeds `timeout` s (killed) gives {"error": ...}."""
     import shutil
     import subprocess
     import tempfile
@@ -1178,7 +1222,11 @@ def live_traffic(args, rows, L, K, timeout=180):
     child = [sys.executable, os.path.abspath(__file__), "--profile", "--steps", "10", "--warmup", "2",
              "--settle-ms", "50", "--total-clients", str(args.total_clients), "--log2-L", str(args.log2_L),
              "--dropout", str(args.dropout)]
-    env = dict(os.environ, TMPDIR="/tmp")
+    if args.weak:
+        child += ["--weak", "--clients-per-gpu", str(args.clients_per_gpu)]
+    if world > 1:
+        child += ["--profile-rank", str(rank), "--profile-world", str(world)]
+    env = child_env(os.environ)
     kib = {}
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -1190,18 +1238,20 @@ def live_traffic(args, rows, L, K, timeout=180):
                 return {"error": f"rocprofv3 --pmc {ctr} did not finish in {timeout} s (killed)"}
             if r.returncode != 0:
                 return {"error": f"rocprofv3 --pmc {ctr} exited {r.returncode}: {r.stderr.strip()[-300:]}"}
-            per = pmc_per_dispatch(d, ctr)
+            name, per = pmc_per_dispatch(d, ctr)
             if not per:
-                return {"error": f"no items_kernel<1 dispatch in the {ctr} pass"}
-            kib[ctr] = (sum(per.values()) / len(per), len(per))
+                return {"error": f"no items_kernel dispatch in the {ctr} pass"}
+            kib[ctr] = (sum(per.values()) / len(per), len(per), name)
     read = 2.0 * kib["FETCH_SIZE"][0] * 1024
     write = kib["WRITE_SIZE"][0] * 1024
     alg = 4.0 * rows * L + 4.0 * L
     return {"bytes": int(read + write), "read_bytes_corrected": int(read), "write_bytes": int(write),
             "algorithmic_bytes": int(alg), "traffic_over_algorithmic": round((read + write) / alg, 4),
             "dispatches": {"FETCH_SIZE": kib["FETCH_SIZE"][1], "WRITE_SIZE": kib["WRITE_SIZE"][1]},
+            "kernel": kib["FETCH_SIZE"][2],
             "source": "this run: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, over bench.py --profile (same workload, "
-                      "this box), FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per items_kernel<1> launch"}
+                      "this box), FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, per launch of the round's kernel"
+                      + (f"; rank {rank} of {world} alone on its GPU" if world > 1 else "")}
 
 
 def committed_cpi():

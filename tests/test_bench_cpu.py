@@ -78,7 +78,8 @@ def test_group_leg_failure_becomes_an_error_field():
 
 def test_pmc_csv_sums_instances_per_dispatch(tmp_path):
     """live_traffic's parser: rocprofv3 --pmc writes one CSV row per counter instance; the bytes of
-    one dispatch are their sum, other kernels and counters are ignored."""
+    one dispatch are their sum; the round's kernel is the items_kernel with the most dispatches (the
+    one-off items_kernel<16> that makes the rows is not mistaken for it); other counters are ignored."""
     d = tmp_path / "pass" / "host"
     d.mkdir(parents=True)
     hdr = "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
@@ -89,7 +90,16 @@ def test_pmc_csv_sums_instances_per_dispatch(tmp_path):
             (2, "void flm::items_kernel<1, true>(...)", "WRITE_SIZE", 7.0)]
     (d / "run_counter_collection.csv").write_text(
         hdr + "".join(f'{a},"{b}",{c},{v}\n' for a, b, c, v in rows))
-    per = bench.pmc_per_dispatch(str(tmp_path / "pass"), "FETCH_SIZE")
-    assert per == {"1": 150.5, "2": 120.0}
-    assert bench.pmc_per_dispatch(str(tmp_path / "pass"), "WRITE_SIZE") == {"2": 7.0}
-    assert bench.pmc_per_dispatch(str(tmp_path / "none"), "FETCH_SIZE") == {}
+    name, per = bench.pmc_per_dispatch(str(tmp_path / "pass"), "FETCH_SIZE")
+    assert name.startswith("void flm::items_kernel<1, ") and per == {"1": 150.5, "2": 120.0}
+    assert bench.pmc_per_dispatch(str(tmp_path / "pass"), "WRITE_SIZE")[1] == {"2": 7.0}
+    assert bench.pmc_per_dispatch(str(tmp_path / "pass"), "FETCH_SIZE", kernel="items_kernel<16,")[1] == {"3": 999.0}
+    assert bench.pmc_per_dispatch(str(tmp_path / "none"), "FETCH_SIZE") == (None, {})
+
+
+def test_pmc_child_env_leaves_the_ranks_group():
+    """A rank's profiling child runs as world 1: torchrun's per-rank variables are dropped."""
+    env = bench.child_env({"RANK": "0", "WORLD_SIZE": "8", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                           "MASTER_PORT": "29500", "TORCHELASTIC_RUN_ID": "x", "PATH": "/usr/bin",
+                           "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert env == {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0", "TMPDIR": "/tmp"}
