@@ -15,6 +15,7 @@
 #   rccltrace    the same script under rocprofv3 --kernel-trace --stats (put it last in a call)
 #   ecpmc:K      rocprofv3 PMC pass (VALU/SALU instructions, wave cycles, waits) of the combine at D = 4
 #                with ec_coop K (1: per-lane field, 2: row field)
+#   pmc:SCRIPT   one rocprofv3 PMC pass (SQ/GRBM issue counters) over python tools/SCRIPT -> TAG_pmc_<name>/
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
 #   py:SCRIPT[:ARG]  python tools/SCRIPT [ARG] (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
@@ -76,6 +77,15 @@ for step in "$@"; do
         -d "$O/${TAG}_ecpmc${step#ecpmc:}" -o run -- python3 "$R/tools/ec_bench.py" --D 4 --T 20 --reps 3 \
         --scalars lagrange --coop "${step#ecpmc:}" > "$O/${TAG}_ecpmc${step#ecpmc:}.log" 2>&1) \
         || { tail -20 "$O/${TAG}_ecpmc${step#ecpmc:}.log"; exit 1; } ;;
+    pmc:*)
+      # one PMC pass (VALU/SALU instructions, waves, wave cycles, busy, waits) over python tools/SCRIPT
+      s=${step#pmc:}
+      n=$(basename "${s%.py}")
+      (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \
+        SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_INSTS_SALU --output-format csv \
+        -d "$O/${TAG}_pmc_$n" -o run -- python3 "$R/tools/$s" > "$O/${TAG}_pmc_$n.log" 2>&1) \
+        || { tail -20 "$O/${TAG}_pmc_$n.log"; exit 1; }
+      tail -2 "$O/${TAG}_pmc_$n.log" ;;
     prof)
       bash tools/gpu_prof.sh "$TAG" || exit 1 ;;
     clock)
