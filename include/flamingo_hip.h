@@ -170,7 +170,7 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              them, the field multiplications of each point doubling and addition spread over
  *              the waves (a shorter latency chain for batches that leave most SIMDs idle); 2:
  *              the same with every field element on a 16-lane row (four products per workgroup,
- *              ~110 instructions per multiplication against ~258).
+ *              ~93 instructions per multiplication against ~258).
  *              Auto: the row kernel up to 20 products per CU, the cooperative kernel up to 128
  *              per CU (one pass of the device), else one lane per product.
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
@@ -182,7 +182,10 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or
  *              mask_hi == L).  That path builds no device seed table: a following
- *              flm_aggregate_dev needs its own flm_seed_table_dev. */
+ *              flm_aggregate_dev needs its own flm_seed_table_dev.
+ *   "client_tiles" 0 (default: auto) | n: 256-slot tiles per workgroup of the one-launch client
+ *              masking (flm_client_mask_dev batches of <= 2^26 mask words); auto fits the grid
+ *              in one generation of resident workgroups. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the
