@@ -90,15 +90,11 @@ int small_round_slots(int B);
 hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
                               const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi,
                               uint32_t ctr0, uint32_t *d_out, uint32_t *d_meta, hipStream_t stream);
-// Client masking with the same kernel (SEG mode): grid (ceil(L/256/tiles), N), row i gets seeds
-// [d_seg[i], d_seg[i+1]) on top of x row i (or the constant `bias` when d_x is NULL); each workgroup
-// runs `tiles` consecutive 256-slot tiles, sized from resident_blocks (> 0: workgroups the chip holds
-// at once, one generation; -n: n tiles each).
+// Client masking with the same kernel (SEG mode): grid (L/256, N), row i gets seeds
+// [d_seg[i], d_seg[i+1]) on top of x row i (or the constant `bias` when d_x is NULL).
 hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, const int64_t *d_seg,
                                    const uint8_t *d_seeds, const int8_t *d_signs, uint64_t L, uint32_t bias,
-                                   uint32_t *d_out, hipStream_t stream, int resident_blocks);
-// workgroups of the SEG kernel one CU holds at once (its LDS / VGPR occupancy)
-hipError_t small_client_mask_blocks_per_cu(int *n);
+                                   uint32_t *d_out, hipStream_t stream);
 uint32_t pair_units_count(int K, uint64_t L, uint32_t *n_tiles);
 hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *d_dst, uint64_t L, uint32_t *d_ws,
                              int groups, hipStream_t stream);

@@ -566,12 +566,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
 // so flm_check_signs keeps working.
 // SEG (client masking, SA_ClientAgent.py:304-324): blockIdx.y is output row i; its seeds are
 // [seg[i], seg[i+1]), its input is row i of `rows` (none: the all-ones input, `bias` = 1), and
-// the row is written at out + i*pitch.  No sign counts (the host validated the signs).  A SEG
-// workgroup runs `tiles` consecutive tiles of its row: a c2 batch (128 clients x 64 tiles, one
-// ChaCha block per lane per tile) as 8,192 one-tile workgroups averaged 4.7 resident waves per SIMD
-// of the 7 its LDS allows (PMC, profiles/r04_c2_client_pmc.json): the workgroups were too short-lived
-// for the dispatcher to keep the CUs full.  launch_small_client_mask sizes `tiles` so the grid fits
-// the chip in one generation.
+// the row is written at out + i*pitch.  No sign counts (the host validated the signs).
 template <int B, bool SEG = false>
 __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__restrict__ rows, uint64_t pitch, int N,
                                                           const uint8_t *__restrict__ seeds,
@@ -579,7 +574,7 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
                                                           uint64_t mask_lo, uint64_t mask_hi, uint32_t ctr0,
                                                           uint32_t *__restrict__ out, uint32_t *__restrict__ meta,
                                                           const int64_t *__restrict__ seg = nullptr,
-                                                          uint32_t bias = 0u, int tiles = 1) {
+                                                          uint32_t bias = 0u) {
     constexpr int T = 16 * B;     // slots per workgroup
     constexpr int SPW = 64 / B;   // seeds per wave per pass
     constexpr int SPP = 4 * SPW;  // seeds per pass
@@ -592,6 +587,7 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
     __shared__ uint32_t lp[G * T];                                  // per-group slot partials (256 words)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t slot0 = (uint64_t)blockIdx.x * T;
     int k_lo = 0, k_hi = K;
     if constexpr (SEG) {
         const uint64_t y = blockIdx.y;
@@ -600,14 +596,7 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
         N = rows ? 1 : 0;
         if (rows) rows += y * pitch;
         out += y * pitch;
-    } else {
-        tiles = 1;
     }
-#pragma unroll 1
-    for (int ti = 0; ti < tiles; ++ti) {
-    const uint64_t slot0 = ((uint64_t)blockIdx.x * tiles + ti) * T;
-    if (slot0 >= L) break;  // workgroup-uniform
-    if (ti > 0) __syncthreads();  // the last tile's combine has read lm / lr / lp
 
     // ---- rows: the first RB of this thread's rows are loaded before the masks
     const int q = tid % Q, rg = tid / Q;
@@ -724,7 +713,6 @@ __global__ __launch_bounds__(256) void small_round_kernel(const uint32_t *__rest
         for (int g = 0; g < G; ++g) total += lp[g * T + tid];
         if (slot0 + tid < L) out[slot0 + tid] = total;
     }
-    }  // tiles
 
     // ---- sign counts (block 0), the same meta layout as seed_schedule_kernel with one part
     if (!SEG && blockIdx.x == 0) {
@@ -970,27 +958,12 @@ hipError_t launch_small_round(int B, const uint32_t *d_rows, uint64_t pitch, int
 
 hipError_t launch_small_client_mask(const uint32_t *d_x, uint64_t pitch, int N, const int64_t *d_seg,
                                    const uint8_t *d_seeds, const int8_t *d_signs, uint64_t L, uint32_t bias,
-                                   uint32_t *d_out, hipStream_t stream, int resident_blocks) {
+                                   uint32_t *d_out, hipStream_t stream) {
     constexpr int B = 16;  // 256-slot tiles: 4 seeds x 16 blocks per wave, 16 seeds per pass
-    const uint64_t tiles_x = (L + 16 * B - 1) / (16 * B);
-    // tiles per workgroup: resident_blocks > 0: the fewest that fit the whole grid in that many
-    // workgroups (one generation: no workgroup waits for a slot, no tail generation runs alone);
-    // resident_blocks = -n: n tiles each (flm_set_tuning "client_tiles")
-    uint64_t per = 1;
-    if (resident_blocks > 0)
-        per = std::max<uint64_t>(1, (tiles_x * (uint64_t)N + (uint64_t)resident_blocks - 1) / (uint64_t)resident_blocks);
-    else if (resident_blocks < 0)
-        per = (uint64_t)(-(int64_t)resident_blocks);
-    per = std::min<uint64_t>(per, std::max<uint64_t>(tiles_x, 1));
-    const dim3 grid((unsigned)((tiles_x + per - 1) / per), (unsigned)N);
+    const dim3 grid((unsigned)((L + 16 * B - 1) / (16 * B)), (unsigned)N);
     hipLaunchKernelGGL((small_round_kernel<B, true>), grid, dim3(256), 0, stream, d_x, pitch, 0, d_seeds, d_signs, 0,
-                       L, (uint64_t)0, L, 0u, d_out, (uint32_t *)nullptr, d_seg, bias, (int)per);
+                       L, (uint64_t)0, L, 0u, d_out, (uint32_t *)nullptr, d_seg, bias);
     return hipGetLastError();
-}
-
-hipError_t small_client_mask_blocks_per_cu(int *n) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, reinterpret_cast<const void *>(small_round_kernel<16, true>),
-                                                        256, 0);
 }
 
 uint32_t pair_units_count(int K, uint64_t L, uint32_t *n_tiles) {

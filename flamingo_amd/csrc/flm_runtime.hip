@@ -131,8 +131,6 @@ struct flm_ctx {
                                 // waves per 4, each element on a 16-lane row (ec_mul_row_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
-    int tune_client_tiles = 0;  // small client masking: 256-slot tiles per workgroup (0: auto, one generation)
-    int client_resident = 0;    // workgroups of small_round_kernel<16, SEG> resident on the chip at once (lazy)
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
                              // 2 same-tile window items (plan_window_same; 0.228 vs 0.188 ms at G = 8, r02_ab_window_same.log)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
@@ -1102,19 +1100,9 @@ int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, 
         std::memcpy(slot->host, seg, seg_bytes);
         if (K > 0) std::memcpy(static_cast<uint8_t *>(slot->host) + seg_bytes, signs, (size_t)K);
         FLM_HIP(ctx, stage_upload(slot, need, s));
-        if (ctx->client_resident == 0) {
-            int cus = 0, per_cu = 0;
-            FLM_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-            FLM_HIP(ctx, flm::small_client_mask_blocks_per_cu(&per_cu));
-            ctx->client_resident = std::max(1, cus * std::max(1, per_cu));
-        }
-        // tiles per workgroup: auto = the grid in one generation of resident workgroups; n = n tiles
-        const int resident = ctx->tune_client_tiles > 0
-                                 ? -ctx->tune_client_tiles : ctx->client_resident;
         const hipError_t e = flm::launch_small_client_mask(
             d_x, pitch, N, slot->dev.as<int64_t>(), d_seeds,
-            reinterpret_cast<const int8_t *>(slot->dev.as<uint8_t>() + seg_bytes), L, d_x ? 0u : 1u, d_out, s,
-            resident);
+            reinterpret_cast<const int8_t *>(slot->dev.as<uint8_t>() + seg_bytes), L, d_x ? 0u : 1u, d_out, s);
         FLM_HIP(ctx, stage_commit(slot, s));
         FLM_HIP(ctx, e);
         ctx->last_items = (int)(((L + 255) / 256) * (uint64_t)N);
@@ -1245,9 +1233,6 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "small") {
         if (value < 0 || value > 2) return fail(ctx, FLM_EINVAL, "small must be 0 (never), 1 (auto) or 2 (when legal)");
         ctx->tune_small = value;
-    } else if (k == "client_tiles") {
-        if (value < 0 || value > 4096) return fail(ctx, FLM_EINVAL, "client_tiles must be 0 (auto) or 1..4096");
-        ctx->tune_client_tiles = value;
     } else if (k == "min_items") {
         if (value < 64 || value > (1 << 20)) return fail(ctx, FLM_EINVAL, "min_items must be in [64, 2^20]");
         ctx->tune_min_items = value;

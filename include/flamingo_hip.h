@@ -182,10 +182,7 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or
  *              mask_hi == L).  That path builds no device seed table: a following
- *              flm_aggregate_dev needs its own flm_seed_table_dev.
- *   "client_tiles" 0 (default: auto) | n: 256-slot tiles per workgroup of the one-launch client
- *              masking (flm_client_mask_dev batches of <= 2^26 mask words); auto fits the grid
- *              in one generation of resident workgroups. */
+ *              flm_aggregate_dev needs its own flm_seed_table_dev. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the

@@ -13,7 +13,6 @@ from flamingo_amd import MaskEngine  # noqa: E402
 from flamingo_amd import params as P  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-TILES = [int(t) for t in os.environ.get("FLM_CLIENT_TILES", "1,0,2,3,4,5,6,8").split(",")]
 N, L = 128, 16384
 eng = MaskEngine(0)
 m = np.frombuffer(b"".join(P.bench_seed("c2-probe", i) for i in range(N)), np.uint8).reshape(N, 32)
@@ -23,17 +22,15 @@ d_cs = torch.from_numpy(cs).cuda()
 rows = torch.empty((N, L), dtype=torch.int32, device="cuda")
 s = torch.cuda.Stream()
 words = int(seg[-1]) * L
-for tiles in TILES:  # flm_set_tuning client_tiles: 0 auto (one generation), n tiles per workgroup
-    eng.set_tuning("client_tiles", tiles)
-    with torch.cuda.stream(s):
-        for _ in range(20):
-            eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=s)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
-            eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=s)
-        e1.record(s)
-        s.synchronize()
-    us = e0.elapsed_time(e1) / reps * 1e3
-    print(f"c2 client masks, client_tiles {tiles}: {int(seg[-1])} seeds, {words / 1e6:.1f} M words, "
-          f"{us:.1f} us per launch, {words / us / 1e3:.1f} G words/s", flush=True)
+with torch.cuda.stream(s):
+    for _ in range(20):
+        eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        eng.client_mask_dev(seg, d_cs, csg, rows, L, stream=s)
+    e1.record(s)
+    s.synchronize()
+us = e0.elapsed_time(e1) / reps * 1e3
+print(f"c2 client masks: {int(seg[-1])} seeds, {words / 1e6:.1f} M words, {us:.1f} us per launch, "
+      f"{words / us / 1e3:.1f} G words/s", flush=True)
