@@ -536,9 +536,10 @@ def main():
                                                          backend=args.dist_backend, comm=comm)}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if G > 1:
-        dist.destroy_process_group()
-    eng.close()
+    # library communicator first, then torch's process group (distributed.shutdown)
+    from flamingo_amd.distributed import shutdown
+    del rnd
+    shutdown(eng)
     return 0 if ok else 1
 
 

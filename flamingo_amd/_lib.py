@@ -48,6 +48,9 @@ SIGNATURES = {
     "flm_ec_combine": (_int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, _u32p]),
     "flm_ec_combine_dev": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _vp, _vp, _vp, _vp]),
     "flm_ec_mul": (_int, [_vp, _u8p, _u8p, _int, _u8p, _u32p]),
+    "flm_hash_to_curve": (_int, [_vp, _u8p, _u32p, _int, _u8p, _u32p]),
+    "flm_hash_to_curve_decimal": (_int, [_vp, ctypes.c_uint32, _int, _u8p, _u32p]),
+    "flm_hash_to_curve_decimal_dev": (_int, [_vp, ctypes.c_uint32, _int, _vp, _vp, _vp]),
     "flm_shamir_combine": (_int, [_vp, _u8p, _u8p, _int, _int, _u8p]),
     "flm_shamir_combine_dev": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
     "flm_pair_units_dev": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp, _int, _int, _vp]),
@@ -61,6 +64,7 @@ SIGNATURES = {
     "flm_comm_unique_id": (_int, [_vp]),
     "flm_comm_init_rank": (_int, [_vp, _int, _int, _vp]),
     "flm_comm_size": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "flm_comm_destroy": (_int, [_vp]),
     "flm_reduce_scatter_dev": (_int, [_vp, _vp, _vp, _sz, _vp]),
     "flm_all_gather_dev": (_int, [_vp, _vp, _vp, _sz, _vp]),
     "flm_group_init": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int)]),

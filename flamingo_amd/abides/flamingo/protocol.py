@@ -32,7 +32,8 @@ _group = None
 _graphs: dict = {}
 _committees: dict = {}
 _pkis: dict = {}
-_h2c: dict = {}
+_h2c: dict = {}           # h_ijt -> point, memoised lookups of the GPU table
+_h2c_table = None         # (out (65536, 64), flags): hash_str_to_curve(str(v)) for every v < 2^16
 _ecdh: dict = {}          # (root, N, min(i,j), max(i,j)) -> 64-byte wire of a_i A_j
 _ecdh_done: set = set()   # batches already computed (graph iterations, committee)
 _clients: dict = {}       # id -> client agent (for the batched ElGamal draws)
@@ -41,7 +42,7 @@ _elgamal: dict = {}       # (root, iteration, id) -> (r list, (deg, 64) rG wire,
 
 def configure(root: bytes | None = None, L: int | None = None, committee: int | None = None):
     """Reset the protocol parameters (between simulations / in tests)."""
-    global root_seed, vector_len, committee_size
+    global root_seed, vector_len, committee_size, _h2c_table
     if root is not None:
         if len(root) != 32:
             raise ValueError("root seed must be 32 bytes")
@@ -57,6 +58,8 @@ def configure(root: bytes | None = None, L: int | None = None, committee: int | 
     _ecdh_done.clear()
     _clients.clear()
     _elgamal.clear()
+    _h2c.clear()                 # the table is the engine's: recomputed with whatever engine is current
+    _h2c_table = None
 
 
 def engine():
@@ -95,18 +98,22 @@ def server_engine():
     device of server_devices(): a DeviceGroup (client-sharded rows, slot-sharded masks, one RCCL
     reduce-scatter) when that is more than one (or FLM_GROUP_RCCL asks for a one-device clique),
     else the process MaskEngine.  Should the group not come up (RCCL missing, a device refused),
-    the server says so and stays on one GPU.  A group replaced while a VectorStore still uses it is
-    not closed here: the store keeps it alive until the store itself is closed (the agent swaps its
-    store at the next iteration boundary, SA_ServiceAgent.reconstruction_clear_pool)."""
+    the server says so and stays on one GPU.  The group is kept while the device list and the
+    requested FLM_GROUP_RCCL flag stay the same (a group of distinct devices always has a clique,
+    so it is the request that is compared, not flm_group_has_rccl).  A group replaced while a
+    VectorStore still uses it is marked retired and closed by that store's close() (the agent swaps
+    its store at the next iteration boundary, SA_ServiceAgent.reconstruction_clear_pool)."""
     global _group
     devs = server_devices()
     force = server_group_rccl()
     if len(devs) == 1 and devs[0] == int(os.environ.get("FLM_DEVICE", "0")) and not force:
         return engine()
-    if _group is None or _group.devices != devs or _group.rccl != force:
+    if _group is None or _group.devices != devs or _group.force_rccl != force:
         from ...engine import DeviceGroup
         if _group is not None:
-            if not _group._stores:
+            if _group._stores:
+                _group.retired = True      # closed by its last VectorStore's close()
+            else:
                 _group.close()
             _group = None
         try:
@@ -167,11 +174,24 @@ def pki(num_clients: int):
 
 def hash_to_curve(h_ijt: str):
     """ecchash.hash_str_to_curve(h_ijt, 2, n, m, L, XMD-SHA256) as the client calls it
-    (SA_ClientAgent.py:283-286).  h_ijt is a decimal string below 2^16, so results are memoised."""
+    (SA_ClientAgent.py:283-286), on the GPU.  h_ijt is str(x & 0xFFFF) (:280), so the first call
+    computes the whole table of the 2^16 possible points in one launch
+    (MaskEngine.hash_to_curve_decimal) and every later call is a lookup; any other message is
+    hashed by its own launch.  Returns the affine point (x, y), or None for infinity."""
+    global _h2c_table
     pt = _h2c.get(h_ijt)
-    if pt is None:
-        from ...crypto import hash_str_to_curve
-        pt = _h2c[h_ijt] = hash_str_to_curve(h_ijt)
+    if pt is not None:
+        return pt
+    if h_ijt.isdigit() and str(int(h_ijt)) == h_ijt and int(h_ijt) < (1 << 16):
+        if _h2c_table is None:
+            _h2c_table = engine().hash_to_curve_decimal(0, 1 << 16)
+        out, fl = _h2c_table
+        row, f = out[int(h_ijt)], int(fl[int(h_ijt)])
+    else:
+        out, fl = engine().hash_to_curve_wire([h_ijt])
+        row, f = out[0], int(fl[0])
+    b = row.tobytes()
+    pt = _h2c[h_ijt] = None if f & 4 else (int.from_bytes(b[:32], "big"), int.from_bytes(b[32:], "big"))
     return pt
 
 

@@ -143,11 +143,15 @@ class SA_ServiceAgent(Agent):
     @vec_sum_partial.setter
     def vec_sum_partial(self, value):
         """Reference-style assignment (e.g. `server.vec_sum_partial = np.zeros(L, uint32)` before
-        reconstruction_process) sets the host copy the getter returns until the next report."""
+        reconstruction_process, as the reference's attribute allows): without a report this
+        iteration, reconstruction_process adds the masks to this value (MaskEngine.mask_accumulate)."""
         if self._store is not None and getattr(self._store, "has_partial", False):
             raise RuntimeError("vec_sum_partial is device-resident after report; assign it before report "
                                "or after the iteration's reset")
-        self._host_partial = np.asarray(value, dtype=self.vector_dtype)
+        v = np.asarray(value)
+        if v.shape != (self.vector_len,):
+            raise RuntimeError("Client sends vector of incorrect length.")   # the guard of :348-349
+        self._host_partial = np.ascontiguousarray(v, dtype=self.vector_dtype)
 
     # ---------------------------------------------------------------- round
     def initialize(self, currentTime):
@@ -312,7 +316,13 @@ class SA_ServiceAgent(Agent):
         # final_sum = partial + cancel + mi  (:538-540, :605), on the GPU(s): every device adds the
         # K masks over its own slot shard of the device-resident S, then the one copy to the host
         t0 = pd.Timestamp("now")
-        self.final_sum = self.store().unmask(seeds, signs)
+        st = self.store()
+        if getattr(st, "has_partial", True):
+            self.final_sum = st.unmask(seeds, signs)
+        else:
+            # no report this iteration: the reference-style assigned partial sum (vec_sum_partial
+            # setter, :540/:605) is the S the masks are added to, on the GPU
+            self.final_sum = param.engine().mask_accumulate(seeds, signs, self._host_partial.copy())
         ms = (pd.Timestamp("now") - t0).total_seconds() * 1e3
         self.gpu_ms.setdefault(self.current_iteration, {})["reconstruction_unmask_wall"] = ms
         self.agent_print(f"reconstruction unmask: {len(seeds)} masks over S on the GPU(s) + D2H, {ms:.3f} ms")

@@ -47,6 +47,7 @@ struct Rccl {
     ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommFinalize)(ncclComm_t) = nullptr;  // optional: RCCL builds before 2.18 lack it
     ncclResult_t (*ReduceScatter)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                   hipStream_t) = nullptr;
     ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -87,6 +88,7 @@ Rccl &rccl_state() {
         FLM_SYM(GroupEnd, "ncclGroupEnd");
         FLM_SYM(GetErrorString, "ncclGetErrorString");
 #undef FLM_SYM
+        r.CommFinalize = reinterpret_cast<decltype(r.CommFinalize)>(dlsym(r.h, "ncclCommFinalize"));
     });
     return r;
 }
@@ -133,10 +135,16 @@ int rccl_missing(flm_ctx *ctx) {
 }  // namespace
 
 namespace flm {
+// Finalize (flushes the communicator's outstanding operations and joins its proxy work) and then
+// destroy, with the context's device current.  Callers have synchronised the device first: the
+// collectives may have been enqueued on streams other than the context's own (a torch comm stream).
 void comm_release(flm_ctx *ctx) {
     CommState *cs = comm_of(ctx);
     if (!cs) return;
-    if (cs->comm && rccl()) (void)rccl()->CommDestroy(cs->comm);
+    if (cs->comm && rccl()) {
+        if (rccl()->CommFinalize) (void)rccl()->CommFinalize(cs->comm);
+        (void)rccl()->CommDestroy(cs->comm);
+    }
     delete cs;
     *flm::rt::comm_slot(ctx) = nullptr;
 }
@@ -211,6 +219,17 @@ int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128
     cs->nranks = n_ranks;
     cs->rank = rank;
     *flm::rt::comm_slot(ctx) = cs;
+    return 0;
+}
+
+int flm_comm_destroy(flm_ctx *ctx) {
+    if (!ctx) return flm::rt::set_error(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (!comm_of(ctx)) return 0;
+    flm::rt::DeviceScope dev_scope_;
+    FLM_HIPC(ctx, dev_scope_.set(flm::rt::device_of(ctx)));
+    // every stream of the device: the collectives may sit on a caller's stream, not the context's
+    FLM_HIPC(ctx, hipDeviceSynchronize());
+    flm::comm_release(ctx);
     return 0;
 }
 

@@ -120,6 +120,10 @@ hipError_t launch_shamir_combine(const uint8_t *d_shares, const uint8_t *d_lambd
                                  hipStream_t stream);
 hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T, int D, int negate,
                             uint8_t *d_points_out, uint8_t *d_digests_out, uint32_t *d_flags, hipStream_t stream);
+// hash_str_to_curve of n messages (d_msgs: n x 64 bytes + d_lens), or of the decimal strings of
+// v0 .. v0+n-1 (d_msgs NULL); d_out n x 64 wire bytes, d_flags n words (written)
+hipError_t launch_hash_to_curve(const uint8_t *d_msgs, const uint32_t *d_lens, uint32_t v0, int n, uint8_t *d_out,
+                                uint32_t *d_flags, hipStream_t stream);
 
 }  // namespace flm
 

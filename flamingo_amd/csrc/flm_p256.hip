@@ -299,8 +299,8 @@ __device__ __forceinline__ Fe from_mont(const Fe &a) {
 #ifndef FLM_INV_BINGCD
 #define FLM_INV_BINGCD 1
 #endif
-#if !FLM_INV_BINGCD
 // a^(p-2): p-2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
+// (0 -> 0, which hash-to-curve's map relies on; ec_finish uses it only with FLM_INV_BINGCD=0)
 __device__ Fe fe_inv(const Fe &a) {
     // x_k = a^(2^k - 1)
     Fe x2 = fe_mul(fe_sqr(a), a);
@@ -339,7 +339,6 @@ __device__ Fe fe_inv(const Fe &a) {
     r = fe_mul(r, a);                       // 1
     return r;
 }
-#endif  // !FLM_INV_BINGCD
 
 // ---- inversion by binary GCD (ec_finish_kernel's one-lane chain)
 // Pornin, "Optimized Binary GCD for Modular Inversion" (eprint 2020/972), Algorithm 2, with
@@ -1715,6 +1714,250 @@ __global__ __launch_bounds__(kEcThreads) void shamir_combine_kernel(const uint8_
     store_be(out + (size_t)i * 32, acc);
 }
 
+// ------------------------------------------------------------- hash to curve
+// The client's pairwise seed group element (SA_ClientAgent.py:275-286): h_ijt, a decimal string
+// below 2^16, goes through util/crypto/ecchash.hash_str_to_curve(msg, count=2, modulus=n, degree=1,
+// blen=48, XMDExpander(DST, sha256, 128)) (:277-283):
+//   uniform = expand_message_xmd(msg, DST, 96)                                   (:90-133)
+//   u_k     = OS2IP(uniform[48k : 48k + 48]) mod n      (the client passes n, not p: :285)  (:50-61)
+//   Q_k     = map_to_curve(u_k)                                                   (:233-275)
+//   H       = Q_0 + Q_1                                                           (:282)
+// One lane per message, Montgomery field of the scalar-multiplication kernels.  map_to_curve is the
+// reference's own simplified-SWU variant with Z = -10: tv1 = (100 u^4 - 10 u^2)^-1 (0 -> 0, the x1 =
+// b/30 branch), x1 = -b/a (1 + tv1), x2 = -10 u^2 x1, y = the first square root of g(x1) else of g(x2).
+// Square roots are a^((p+1)/4) (p = 3 mod 4): the root the host restatement (flamingo_amd/crypto.py)
+// takes first for libnum's sqrtmod -- the one convention that stays "parity unpinned" (DESIGN.md).
+// The sgn0 step (:271-272) flips y only when exactly one of u, y is zero.  The whole table of the
+// protocol's 2^16 inputs is one launch (flm_hash_to_curve_decimal).
+constexpr int kH2cMaxMsg = 64;
+__device__ constexpr uint32_t kAm[8] = {0xfffffffcu, 0xffffffffu, 0xffffffffu, 0x00000003u,
+                                        0x00000000u, 0x00000000u, 0x00000004u, 0xfffffffcu};  // a R (a = -3)
+__device__ constexpr uint32_t kC1m[8] = {0x6341949fu, 0x9d899fcbu, 0x7d816585u, 0x8efaac9au,
+                                         0xa7b5ba47u, 0xa1e0b58eu, 0x01826d67u, 0xf4100209u};  // (-b/a) R
+__device__ constexpr uint32_t kC2m[8] = {0xf0535ba9u, 0x5c8dc32du, 0x8c8cf08du, 0xc17f77a9u,
+                                         0x43f892a0u, 0x7696788eu, 0x99c03e24u, 0x98680033u};  // (b/30) R
+__device__ constexpr uint32_t k10m[8] = {0x0000000au, 0x00000000u, 0x00000000u, 0xfffffff6u,
+                                         0xffffffffu, 0xffffffffu, 0xfffffff5u, 0x00000009u};  // 10 R
+__device__ constexpr uint32_t k100m[8] = {0x00000064u, 0x00000000u, 0x00000000u, 0xffffff9cu,
+                                          0xffffffffu, 0xffffffffu, 0xffffff9bu, 0x00000063u};  // 100 R
+__device__ constexpr uint32_t kNeg10m[8] = {0xfffffff5u, 0xffffffffu, 0xffffffffu, 0x0000000au,
+                                            0x00000000u, 0x00000000u, 0x0000000bu, 0xfffffff5u};  // -10 R
+__device__ constexpr uint32_t kNc[7] = {0x039cdaafu, 0x0c46353du, 0x58e8617bu, 0x43190552u,
+                                        0x00000000u, 0x00000000u, 0xffffffffu};  // 2^256 - n (< 2^224)
+// ecchash.test_dst("P256_XMD:SHA-256_SSWU_RO_") || I2OSP(44, 1): DST_prime of :104
+__device__ constexpr uint8_t kDstPrime[45] = {'Q', 'U', 'U', 'X', '-', 'V', '0', '1', '-', 'C', 'S', '0', '2', '-', 'w',
+                                              'i', 't', 'h', '-', 'P', '2', '5', '6', '_', 'X', 'M', 'D', ':', 'S', 'H',
+                                              'A', '-', '2', '5', '6', '_', 'S', 'S', 'W', 'U', '_', 'R', 'O', '_', 44};
+
+// SHA-256 fed byte by byte (the messages are short and their layout depends on the message length)
+struct Sha256 {
+    uint32_t h[8];
+    uint32_t w[16];
+    uint32_t n;      // bytes in w
+    uint32_t total;  // bytes hashed
+};
+
+__device__ __forceinline__ void sha_init(Sha256 &s) {
+    const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab,
+                            0x5be0cd19};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.h[i] = iv[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s.w[i] = 0;
+    s.n = 0;
+    s.total = 0;
+}
+
+__device__ void sha_put(Sha256 &s, uint32_t b) {
+    s.w[s.n >> 2] |= (b & 0xffu) << (24 - 8 * (s.n & 3));
+    ++s.total;
+    if (++s.n == 64) {
+        sha256_block(s.h, s.w);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s.w[i] = 0;
+        s.n = 0;
+    }
+}
+
+__device__ void sha_put_dst(Sha256 &s) {
+#pragma unroll 1
+    for (int i = 0; i < 45; ++i) sha_put(s, kDstPrime[i]);
+}
+
+// the digest as 8 big-endian words (word k = bytes 4k..4k+3)
+__device__ void sha_final(Sha256 &s, uint32_t (&out)[8]) {
+    const uint64_t bits = (uint64_t)s.total * 8;
+    sha_put(s, 0x80);
+#pragma unroll 1
+    while (s.n != 56) sha_put(s, 0);
+#pragma unroll 1
+    for (int i = 7; i >= 0; --i) sha_put(s, (uint32_t)(bits >> (8 * i)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = s.h[i];
+}
+
+// 384-bit big-endian words u[0..11] mod n: fold t = lo + hi (2^256 mod n) until t < 2^256 (at most
+// 7 folds for any 384-bit input: the high part shrinks by >= 31 bits a fold), then one subtraction
+__device__ Fe mod_n_384(const uint32_t *u) {
+    uint32_t t[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) t[i] = u[11 - i];
+#pragma unroll 1
+    for (int it = 0; it < 7; ++it) {
+        uint32_t hi[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            hi[i] = t[8 + i];
+            t[8 + i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint64_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) {
+                c = (uint64_t)hi[i] * kNc[j] + t[i + j] + (c >> 32);
+                t[i + j] = (uint32_t)c;
+            }
+            c >>= 32;
+#pragma unroll
+            for (int k = i + 7; k < 12; ++k) {
+                c += t[k];
+                t[k] = (uint32_t)c;
+                c >>= 32;
+            }
+        }
+    }
+    uint32_t d[8], b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = __builtin_subc(t[i], kN[i], b, &b);
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = b ? t[i] : d[i];  // no borrow: t >= n
+    return r;
+}
+
+__device__ __forceinline__ Fe fe_sqr_n(Fe a, int n) {
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) a = fe_sqr(a);
+    return a;
+}
+
+// a^((p+1)/4), (p+1)/4 = (2^32 - 1) 2^222 + 2^190 + 2^94: 253 squarings, 7 multiplications
+__device__ Fe fe_sqrt_cand(const Fe &a) {
+    const Fe x2 = fe_mul(fe_sqr(a), a);
+    const Fe x4 = fe_mul(fe_sqr_n(x2, 2), x2);
+    const Fe x8 = fe_mul(fe_sqr_n(x4, 4), x4);
+    const Fe x16 = fe_mul(fe_sqr_n(x8, 8), x8);
+    const Fe x32 = fe_mul(fe_sqr_n(x16, 16), x16);
+    Fe r = fe_mul(fe_sqr_n(x32, 32), a);
+    r = fe_mul(fe_sqr_n(r, 96), a);
+    return fe_sqr_n(r, 94);
+}
+
+// map_to_curve (ecchash.py:233-275) of u (canonical, < n < p), affine Montgomery (x, y); bad = neither
+// g(x1) nor g(x2) had a root (cannot happen for this map; flagged rather than assumed)
+__device__ void h2c_map(const Fe &u_plain, Fe &x, Fe &y, bool &bad) {
+    const Fe u = to_mont(u_plain);
+    const Fe u2 = fe_sqr(u);
+    const Fe u4 = fe_sqr(u2);
+    const Fe den = fe_sub(fe_mul(fe_const(k100m), u4), fe_mul(fe_const(k10m), u2));
+    const Fe tv1 = fe_inv(den);                                   // 0 -> 0 (the :247-248 branch)
+    Fe x1 = fe_mul(fe_const(kC1m), fe_add(fe_const(kOne), tv1));
+    if (fe_is_zero(tv1)) x1 = fe_const(kC2m);
+    const Fe gx1 = fe_add(fe_mul(x1, fe_add(fe_sqr(x1), fe_const(kAm))), fe_const(kBm));
+    const Fe x2 = fe_mul(fe_const(kNeg10m), fe_mul(u2, x1));
+    const Fe gx2 = fe_add(fe_mul(x2, fe_add(fe_sqr(x2), fe_const(kAm))), fe_const(kBm));
+    const Fe y1 = fe_sqrt_cand(gx1);
+    const bool sq1 = fe_eq(fe_sqr(y1), gx1);
+    const Fe y2 = fe_sqrt_cand(gx2);
+    bad = !sq1 && !fe_eq(fe_sqr(y2), gx2);
+    x = sq1 ? x1 : x2;
+    y = sq1 ? y1 : y2;
+    if (fe_is_zero(u_plain) != fe_is_zero(y)) y = fe_neg(y);    // sgn0(u) != sgn0(y), :271-272
+}
+
+// msgs: n x kH2cMaxMsg bytes (message i in its first lens[i] bytes), or NULL for the decimal
+// strings of v0 + i (str(h_ijt), SA_ClientAgent.py:280).  out: n x 64 wire bytes (infinity: zeros,
+// flags bit 2); flags bit 3: no square root (not expected).
+__global__ __launch_bounds__(kEcThreads) void hash_to_curve_kernel(const uint8_t *__restrict__ msgs,
+                                                                   const uint32_t *__restrict__ lens, uint32_t v0,
+                                                                   int n, uint8_t *__restrict__ out,
+                                                                   uint32_t *__restrict__ flags) {
+    const int i = blockIdx.x * kEcThreads + threadIdx.x;
+    if (i >= n) return;
+    uint8_t msg[kH2cMaxMsg];
+    int m = 0;
+    if (msgs) {
+        m = (int)lens[i];
+#pragma unroll 1
+        for (int k = 0; k < m; ++k) msg[k] = msgs[(size_t)i * kH2cMaxMsg + k];
+    } else {
+        uint32_t v = v0 + (uint32_t)i;
+        uint8_t dig[10];
+        int nd = 0;
+#pragma unroll 1
+        do {
+            dig[nd++] = (uint8_t)('0' + v % 10);
+            v /= 10;
+        } while (v);
+#pragma unroll 1
+        for (int k = 0; k < nd; ++k) msg[k] = dig[nd - 1 - k];
+        m = nd;
+    }
+    // b_0 = H(Z_pad || msg || I2OSP(96, 2) || I2OSP(0, 1) || DST_prime)   (:113-114)
+    Sha256 s;
+    sha_init(s);
+    sha256_block(s.h, s.w);  // Z_pad: one all-zero block (s.w is zero)
+    s.total = 64;
+#pragma unroll 1
+    for (int k = 0; k < m; ++k) sha_put(s, msg[k]);
+    sha_put(s, 0);
+    sha_put(s, 96);
+    sha_put(s, 0);
+    sha_put_dst(s);
+    uint32_t b0[8], bi[8], uni[24];
+    sha_final(s, b0);
+    // b_1 = H(b_0 || 1 || DST_prime), b_i = H((b_0 ^ b_{i-1}) || i || DST_prime)   (:115-117)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bi[k] = 0;
+#pragma unroll 1
+    for (int blk = 1; blk <= 3; ++blk) {
+        sha_init(s);
+#pragma unroll 1
+        for (int k = 0; k < 32; ++k) sha_put(s, (b0[k >> 2] ^ bi[k >> 2]) >> (24 - 8 * (k & 3)));
+        sha_put(s, (uint32_t)blk);
+        sha_put_dst(s);
+        sha_final(s, bi);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) uni[(blk - 1) * 8 + k] = bi[k];
+    }
+    Fe x0, y0, x1, y1;
+    bool bad0, bad1;
+    h2c_map(mod_n_384(uni), x0, y0, bad0);
+    h2c_map(mod_n_384(uni + 12), x1, y1, bad1);
+    Jac Q0, Q1;
+    Q0.X = x0;
+    Q0.Y = y0;
+    Q0.Z = fe_const(kOne);
+    Q1.X = x1;
+    Q1.Y = y1;
+    Q1.Z = fe_const(kOne);
+    const Jac R = jac_add(Q0, Q1);                                 // Q0 + Q1 (:282), P == +-Q handled
+    uint32_t fl = (bad0 || bad1) ? 8u : 0u;
+    Fe x = {}, y = {};
+    if (fe_is_zero(R.Z)) {
+        fl |= 4u;
+    } else {
+        const Fe zi = fe_inv(R.Z);
+        const Fe zi2 = fe_sqr(zi);
+        x = from_mont(fe_mul(R.X, zi2));
+        y = from_mont(fe_mul(R.Y, fe_mul(zi2, zi)));
+    }
+    store_be(out + (size_t)i * 64, x);
+    store_be(out + (size_t)i * 64 + 32, y);
+    flags[i] = fl;
+}
+
 }  // namespace
 
 template <int TPB, int WPE>
@@ -1790,6 +2033,14 @@ hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T,
     dim3 grid((D + per_group - 1) / per_group);
     hipLaunchKernelGGL(ec_finish_kernel, grid, dim3(kEcThreads), 0, stream, d_base, d_jac, T, D, negate,
                        d_points_out, d_digests_out, d_flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_to_curve(const uint8_t *d_msgs, const uint32_t *d_lens, uint32_t v0, int n, uint8_t *d_out,
+                                uint32_t *d_flags, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hash_to_curve_kernel, dim3((unsigned)((n + kEcThreads - 1) / kEcThreads)), dim3(kEcThreads), 0,
+                       stream, d_msgs, d_lens, v0, n, d_out, d_flags);
     return hipGetLastError();
 }
 

@@ -1450,6 +1450,62 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     return 0;
 }
 
+static int h2c_run(flm_ctx *ctx, const uint8_t *msgs, const uint32_t *lens, uint32_t v0, int n, uint8_t *out,
+                   uint32_t *flags_out) {
+    FLM_ON_DEVICE(ctx);
+    hipStream_t s = ctx->stream;
+    FLM_HIP(ctx, ctx->ec_out.reserve((size_t)n * 64));
+    FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)n * 4));
+    if (msgs) {
+        FLM_HIP(ctx, ctx->ec_in.reserve((size_t)n * 64));
+        FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)n * 4));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, msgs, (size_t)n * 64, hipMemcpyHostToDevice, s));
+        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    FLM_HIP(ctx, flm::launch_hash_to_curve(msgs ? ctx->ec_in.as<uint8_t>() : nullptr,
+                                           msgs ? ctx->ec_scal.as<uint32_t>() : nullptr, v0, n,
+                                           ctx->ec_out.as<uint8_t>(), ctx->ec_flags.as<uint32_t>(), s));
+    std::vector<uint32_t> fl(n);
+    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->ec_out.p, (size_t)n * 64, hipMemcpyDeviceToHost, s));
+    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
+    for (int i = 0; i < n; ++i)
+        if (fl[i] & 8u) return fail(ctx, FLM_EINVAL, "message %d: map_to_curve found no square root", i);
+    return 0;
+}
+
+int flm_hash_to_curve(flm_ctx *ctx, const uint8_t *msgs, const uint32_t *lens, int n, uint8_t *out,
+                      uint32_t *flags_out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, 1, n)) return rc;
+    if (n == 0) return 0;
+    if (!msgs || !lens || !out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    for (int i = 0; i < n; ++i)
+        if (lens[i] > 64) return fail(ctx, FLM_EINVAL, "message %d is %u bytes (at most 64)", i, lens[i]);
+    return h2c_run(ctx, msgs, lens, 0, n, out, flags_out);
+}
+
+int flm_hash_to_curve_decimal(flm_ctx *ctx, uint32_t v0, int n, uint8_t *out, uint32_t *flags_out) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, 1, n)) return rc;
+    if (n == 0) return 0;
+    if (!out) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if ((uint64_t)v0 + (uint64_t)n > (1ull << 32)) return fail(ctx, FLM_EINVAL, "v0 + n exceeds 2^32");
+    return h2c_run(ctx, nullptr, nullptr, v0, n, out, flags_out);
+}
+
+int flm_hash_to_curve_decimal_dev(flm_ctx *ctx, uint32_t v0, int n, uint8_t *d_out, uint32_t *d_flags, void *stream) {
+    if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
+    if (int rc = ec_dims(ctx, 1, n)) return rc;
+    if (n == 0) return 0;
+    if (!d_out || !d_flags) return fail(ctx, FLM_EINVAL, "NULL argument");
+    if ((uint64_t)v0 + (uint64_t)n > (1ull << 32)) return fail(ctx, FLM_EINVAL, "v0 + n exceeds 2^32");
+    FLM_ON_DEVICE(ctx);
+    FLM_HIP(ctx, flm::launch_hash_to_curve(nullptr, nullptr, v0, n, d_out, d_flags, static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
 void *flm_host_alloc(size_t bytes) {
     void *p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;

@@ -110,13 +110,14 @@ class ShardedReconstruction:
 
     def _ec_combine(self, c1, shares, lambdas, seeds, flags):
         """The rank's pair chunk on the side stream; on confined CUs with the ec_coop kernel."""
+        prev = self.eng.get_tuning("ec_coop")
         if self.ec_cus > 0:
             self.eng.set_tuning("ec_coop", self.ec_coop)
         try:
             self.eng.ec_combine_dev(c1, shares, lambdas, seeds, flags, stream=self.side)
         finally:
             if self.ec_cus > 0:
-                self.eng.set_tuning("ec_coop", -1)
+                self.eng.set_tuning("ec_coop", prev)          # the caller's own setting, not auto
 
     def _pass_begin(self, ready, main):
         """The stream Shamir and the self-mask pass run on: the caller's, or (ec_cus > 0) the

@@ -94,6 +94,43 @@ def init_rccl(engine, group=None):
     return world, rank
 
 
+def shutdown(*owners, group_initialized: bool | None = None):
+    """Ordered teardown of one process's RCCL users; every rank calls it at the end of its run.
+
+    torch's nccl process group and the library's communicators come from the same librccl.so
+    (flm_comm.hip resolves the copy torch loaded).  Destroying torch's group first and leaving the
+    library communicator to flm_free -- or to a __del__ at interpreter exit -- ended the process in
+    an exit-time destructor (__cxa_finalize) after every check had passed (the rccl
+    clique smoke under rocprofv3 with the nccl backend).  The order here:
+      1. synchronise the device (the collectives may sit on a comm stream of their own);
+      2. finalize + destroy every library communicator (MaskEngine.comm_destroy; a DeviceGroup's
+         clique is destroyed by closing the group);
+      3. a barrier, so no rank tears down torch's group while a peer is still in step 2;
+      4. torch.distributed.destroy_process_group();
+      5. close every owner (contexts, CU streams, device buffers) and collect, so nothing of ours is
+         left for a finalizer at interpreter exit.
+    owners: MaskEngine / DeviceGroup / anything with close(); a VectorStore must come before the
+    group it lives on."""
+    import gc
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    from .engine import MaskEngine
+    rest = []
+    for o in owners:
+        if isinstance(o, MaskEngine):
+            o.comm_destroy()
+            rest.append(o)
+        elif o is not None:
+            o.close()                    # stores, then the groups they live on (clique destroyed here)
+    init = dist.is_initialized() if group_initialized is None else group_initialized
+    if init:
+        dist.barrier()
+        dist.destroy_process_group()
+    for o in rest:
+        o.close()
+    gc.collect()
+
+
 def _torch_stream(stream):
     if stream is None or isinstance(stream, torch.cuda.Stream):
         return stream

@@ -117,9 +117,19 @@ class MaskEngine:
         if rc != 0:
             raise RuntimeError(f"{what}: {self.lib.flm_last_error(self.ctx).decode()} (code {rc})")
 
+    # flm_set_tuning defaults (include/flamingo_hip.h), for get_tuning before any set_tuning
+    TUNING_DEFAULTS = {"variant": -1, "subtiles": 0, "pairing": 1, "min_items": 1024, "ec_threads": 64,
+                       "ec_waves": 1, "ec_coop": -1, "ec_terms": 1, "ec_spread": 0, "small": 1}
+
     def set_tuning(self, key: str, value: int):
         """A/B knobs: variant (-1 auto, 0..3) and subtiles (0 auto, 1, 4, 16)."""
         self._check(self.lib.flm_set_tuning(self.ctx, key.encode(), int(value)), f"flm_set_tuning({key})")
+        self.__dict__.setdefault("_tuning", {})[key] = int(value)
+
+    def get_tuning(self, key: str) -> int:
+        """The value set_tuning last gave `key` on this engine (else the library default)."""
+        t = self.__dict__.get("_tuning", {})
+        return t[key] if key in t else self.TUNING_DEFAULTS[key]
 
     def last_plan(self) -> dict:
         v = [ctypes.c_int() for _ in range(4)]
@@ -157,6 +167,13 @@ class MaskEngine:
         """Attach an RCCL communicator (flm_comm_init_rank; collective over all ranks)."""
         uid = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
         self._check(self.lib.flm_comm_init_rank(self.ctx, int(n_ranks), int(rank), uid), "flm_comm_init_rank")
+
+    def comm_destroy(self):
+        """Synchronise the device, then finalize + destroy the attached RCCL communicator
+        (flm_comm_destroy; a no-op without one).  distributed.shutdown calls this on every rank
+        before torch.distributed's process group is destroyed."""
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self._check(self.lib.flm_comm_destroy(self.ctx), "flm_comm_destroy")
 
     def comm_size(self):
         """(n_ranks, rank) of the attached communicator, (1, 0) without one."""
@@ -381,6 +398,46 @@ class MaskEngine:
         if n:
             self._check(self.lib.flm_ec_mul(self.ctx, p_u8(pw), p_u8(sw), n, p_u8(out), p_u32(fl)), "flm_ec_mul")
         return out, fl
+
+    def hash_to_curve_wire(self, msgs):
+        """ecchash.hash_str_to_curve(msg, 2, n, 1, 48, XMD SHA-256) of each message (str or bytes,
+        <= 64 bytes) on the GPU (flm_hash_to_curve).  Returns (out (n, 64) uint8 wire x||y,
+        flags (n,) uint32; bit 2 = infinity)."""
+        raw = [m.encode() if isinstance(m, str) else bytes(m) for m in msgs]
+        n = len(raw)
+        buf = np.zeros((max(n, 1), 64), np.uint8)
+        lens = np.zeros(max(n, 1), np.uint32)
+        for i, m in enumerate(raw):
+            if len(m) > 64:
+                raise RuntimeError(f"message {i} is {len(m)} bytes (at most 64)")
+            buf[i, :len(m)] = np.frombuffer(m, np.uint8)
+            lens[i] = len(m)
+        out = np.zeros((n, 64), np.uint8)
+        fl = np.zeros(n, np.uint32)
+        if n:
+            self._check(self.lib.flm_hash_to_curve(self.ctx, p_u8(buf), p_u32(lens), n, p_u8(out), p_u32(fl)),
+                        "flm_hash_to_curve")
+        return out, fl
+
+    def hash_to_curve_decimal(self, v0: int = 0, n: int = 1 << 16):
+        """hash_str_to_curve(str(v)) for v in [v0, v0 + n) in one launch (flm_hash_to_curve_decimal):
+        with the defaults, every h_ijt a client can hash (SA_ClientAgent.py:280).  (out, flags) as
+        hash_to_curve_wire."""
+        out = np.zeros((n, 64), np.uint8)
+        fl = np.zeros(n, np.uint32)
+        if n:
+            self._check(self.lib.flm_hash_to_curve_decimal(self.ctx, int(v0), int(n), p_u8(out), p_u32(fl)),
+                        "flm_hash_to_curve_decimal")
+        return out, fl
+
+    def hash_to_curve_decimal_dev(self, v0: int, n: int, out, flags, stream=None):
+        """Device form: out (n, 64) uint8 and flags (n,) int32/uint32 CUDA tensors; enqueued on `stream`."""
+        _dev_bytes(out, "out", 64, n)
+        _dev_bytes(flags, "flags", 1, n, 4)
+        self._check(self.lib.flm_hash_to_curve_decimal_dev(self.ctx, int(v0), int(n), out.data_ptr(), flags.data_ptr(),
+                                                           self._stream_handle(stream)),
+                    "flm_hash_to_curve_decimal_dev")
+        return out, flags
 
     def ec_mul(self, points, scalars) -> list:
         """[k_i * P_i] for affine points (x, y) and integer scalars (flm_ec_mul).
@@ -613,7 +670,9 @@ class DeviceGroup:
         self.n = len(devices)
         self.loopback = bool(self.lib.flm_group_is_loopback(g))
         self.rccl = bool(self.lib.flm_group_has_rccl(g))
+        self.force_rccl = bool(force_rccl)  # as requested (a group of distinct devices has a clique anyway)
         self._stores = 0                    # live VectorStores on this group (close() refuses while > 0)
+        self.retired = False                # replaced while a store still used it: its last store closes it
         self.engines = [MaskEngine(d, _ctx=self.lib.flm_group_ctx(g, r)) for r, d in enumerate(devices)]
 
     def close(self):

@@ -61,6 +61,8 @@ class VectorStore:
             self.h = None
             if self._grp is not None:
                 self._grp._stores -= 1
+                if self._grp._stores == 0 and self._grp.retired:
+                    self._grp.close()              # a group replaced under this store (protocol.server_engine)
 
     def __del__(self):
         try:

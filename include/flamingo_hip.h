@@ -250,6 +250,22 @@ int flm_shamir_combine_dev(flm_ctx *ctx, const uint8_t *d_shares, const uint8_t 
  * (SA_ClientAgent.py:256-263), ElGamal (:434-447) and decryption-share
  * (:397-400) products, n independent elements per call. */
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out);
+/* Hash to curve, replacing util/crypto/ecchash.hash_str_to_curve (:277-283) as the client calls
+ * it for its pairwise seed group element (SA_ClientAgent.py:283-286): expand_message_xmd with
+ * SHA-256 and DST "QUUX-V01-CS02-with-P256_XMD:SHA-256_SSWU_RO_" to 96 bytes (:90-133), two field
+ * elements OS2IP(48 bytes) mod n (the client passes the group order as the modulus, :285;
+ * hash_to_field :50-61), the reference's map_to_curve of each (:233-275), and their sum (:282).
+ * flm_hash_to_curve: msgs n x 64 bytes, message i in its first lens[i] <= 64 bytes.
+ * flm_hash_to_curve_decimal: the messages are str(v) for v in [v0, v0 + n) -- the client's h_ijt is
+ * str(x & 0xFFFF) (:280), so v0 = 0, n = 65536 is every value it can hash: one launch.
+ * out: n x 64 wire bytes; flags bit 2: the sum is the point at infinity (out zeros); FLM_EINVAL if
+ * a map found no square root (flags bit 3; not expected).  _dev: device buffers, enqueued on
+ * `stream`, flags written but not checked.  Square roots are a^((p+1)/4): libnum's sqrtmod root
+ * order is assumed to yield that root first (the one convention not pinned by the reference). */
+int flm_hash_to_curve(flm_ctx *ctx, const uint8_t *msgs, const uint32_t *lens, int n, uint8_t *out,
+                      uint32_t *flags_out);
+int flm_hash_to_curve_decimal(flm_ctx *ctx, uint32_t v0, int n, uint8_t *out, uint32_t *flags_out);
+int flm_hash_to_curve_decimal_dev(flm_ctx *ctx, uint32_t v0, int n, uint8_t *d_out, uint32_t *d_flags, void *stream);
 
 /* ------------------------------------------------ CU-partitioned streams */
 
@@ -286,8 +302,14 @@ int flm_client_bounds(int N, int n_ranks, int rank, int *c0, int *c1);
  * returns 1 when no communicator is attached (then *n_ranks = 1, *rank = 0).
  * flm_rccl_available: 1 when RCCL could be loaded (dlopen) and every symbol
  * resolved, else 0 (reason in flm_last_error(NULL)); local, not collective, so
- * every rank can agree on it before any rank enters flm_comm_init_rank. */
+ * every rank can agree on it before any rank enters flm_comm_init_rank.
+ * flm_comm_destroy: synchronise the context's device, then ncclCommFinalize + ncclCommDestroy
+ * the attached communicator (no-op without one); the context stays usable.  Call it on every
+ * rank BEFORE the process's other RCCL users (torch.distributed's nccl process group) are torn
+ * down -- the teardown order of distributed.shutdown -- so no library communicator is left for
+ * an exit-time destructor. */
 int flm_rccl_available(void);
+int flm_comm_destroy(flm_ctx *ctx);
 int flm_comm_unique_id(uint8_t id_out[128]);
 int flm_comm_init_rank(flm_ctx *ctx, int n_ranks, int rank, const uint8_t id[128]);
 int flm_comm_size(flm_ctx *ctx, int *n_ranks, int *rank);

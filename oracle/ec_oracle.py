@@ -10,7 +10,13 @@ imported by the product path.  Restates, in plain affine integer arithmetic:
 * the Lagrange coefficients of points_to_secret_int
   (util/crypto/secretsharing/polynomials.py modular_lagrange_interpolation, at x = 0, mod n);
 * ElGamal encryption (SA_ClientAgent.py:434-447): c0 = r*G, c1 = h + r*pk;
-* committee decryption shares (SA_ClientAgent.py:397-400): share = sk_j * c0.
+* committee decryption shares (SA_ClientAgent.py:397-400): share = sk_j * c0;
+* hash to curve as the client calls it (SA_ClientAgent.py:283-286):
+  util/crypto/ecchash.py expand_message_xmd (:90-133, SHA-256), hash_to_field (:50-61, with
+  modulus = n), map_to_curve (:233-275), hash_str_to_curve = Q0 + Q1 (:277-283).  Checker for
+  flm_hash_to_curve*; its square root takes a^((p+1)/4) first for libnum's sqrtmod (absent here,
+  so that root order is "parity unpinned"; every other step is pinned by the h2c points of the
+  reference's own runs in tests/golden/ref_golden.npz and by tests/golden/h2c_golden.json).
 
 Pins: tests/test_ec_cpu.py checks this arithmetic against OpenSSL's
 independent P-256 (EC_POINT_mul / EC_POINT_add) and against the group law
@@ -102,3 +108,53 @@ def combine(c1, shares_by_term, lambdas, negate: bool = True):
 
 def elgamal_encrypt(pk, h, r: int):
     return mul(r), add(h, mul(r, pk))
+
+
+# ------------------------------------------------------------- hash to curve
+DST = b"QUUX-V01-CS02-with-P256_XMD:SHA-256_SSWU_RO_"      # ecchash.test_dst("P256_XMD:SHA-256_SSWU_RO_")
+
+
+def expand_message_xmd(msg: bytes, dst: bytes, len_in_bytes: int) -> bytes:
+    """ecchash.py:90-133 with hashlib.sha256 (b_in_bytes 32, r_in_bytes 64)."""
+    ell = (len_in_bytes + 31) // 32
+    dst_prime = dst + bytes([len(dst)])
+    b0 = hashlib.sha256(bytes(64) + msg + len_in_bytes.to_bytes(2, "big") + b"\x00" + dst_prime).digest()
+    b = [hashlib.sha256(b0 + b"\x01" + dst_prime).digest()]
+    for i in range(1, ell):
+        b.append(hashlib.sha256(bytes(x ^ y for x, y in zip(b0, b[-1])) + bytes([i + 1]) + dst_prime).digest())
+    return b"".join(b)[:len_in_bytes]
+
+
+def map_to_curve(u: int):
+    """ecchash.py:233-275 (Z = -10); a^((p+1)/4) as the first root of libnum.sqrtmod."""
+    den = (100 * pow(u, 4, P) - 10 * pow(u, 2, P)) % P
+    tv1 = pow(den, P - 2, P)                       # libnum.invmod; 0 -> 0 takes the :247-248 branch
+    x1 = ((-B * pow(A, -1, P)) * (1 + tv1)) % P
+    if tv1 == 0:
+        x1 = B * pow(30, -1, P) % P
+    gx1 = (x1 ** 3 + A * x1 + B) % P
+    x2 = (-10 * pow(u, 2, P) * x1) % P
+    gx2 = (x2 ** 3 + A * x2 + B) % P
+    y = pow(gx1, (P + 1) // 4, P)
+    x = x1
+    if y * y % P != gx1:
+        x, y = x2, pow(gx2, (P + 1) // 4, P)
+    if (u <= 0) != (y <= 0):                       # sgn0(u) != sgn0(y), :227-232, :271-272
+        y = (-y) % P
+    return (x, y)
+
+
+def hash_str_to_curve(msg) -> tuple | None:
+    """ecchash.hash_str_to_curve(msg, 2, n, 1, 48, XMDExpander(DST, sha256, 128))."""
+    m = msg.encode() if isinstance(msg, str) else bytes(msg)
+    ub = expand_message_xmd(m, DST, 96)
+    u0, u1 = (int.from_bytes(ub[48 * i: 48 * i + 48], "big") % N for i in range(2))
+    return add(map_to_curve(u0), map_to_curve(u1))
+
+
+def h2c_table_digest(points) -> str:
+    """SHA-256 over the 64-byte wire encodings of a table of points (infinity = 64 zeros)."""
+    h = hashlib.sha256()
+    for pt in points:
+        h.update(wire(pt))
+    return h.hexdigest()

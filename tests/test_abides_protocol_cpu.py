@@ -55,7 +55,40 @@ class OracleStore:
         return O.aggregate_unmask(self.S[None], sd, np.asarray(signs, np.int8), L=self.L)
 
 
+class LazyH2C:
+    """The (65536, 64) hash-to-curve table of hash_to_curve_decimal, computed row by row on demand
+    by the pure-Python restatement (the whole table would take ~30 s of Python)."""
+
+    def __init__(self, v0):
+        self.v0, self.rows = v0, {}
+
+    def _pt(self, i):
+        if i not in self.rows:
+            self.rows[i] = E.hash_str_to_curve(str(self.v0 + i))
+        return self.rows[i]
+
+    def table(self):
+        outer = self
+
+        class Rows:
+            def __getitem__(self, i):
+                return np.frombuffer(E.wire(outer._pt(int(i))), np.uint8)
+
+        class Flags:
+            def __getitem__(self, i):
+                return 4 if outer._pt(int(i)) is None else 0
+        return Rows(), Flags()
+
+
 class OracleEngine:
+    def hash_to_curve_decimal(self, v0=0, n=1 << 16):
+        return LazyH2C(v0).table()
+
+    def hash_to_curve_wire(self, msgs):
+        pts = [E.hash_str_to_curve(m) for m in msgs]
+        return (np.stack([np.frombuffer(E.wire(p), np.uint8) for p in pts]),
+                np.array([4 if p is None else 0 for p in pts], np.uint32))
+
     def vector_store(self, L, capacity):
         return OracleStore(L)
 

@@ -111,17 +111,18 @@ def test_reconstruction_from_reference_shares(eng, ref, refnpz):
         assert digest(out[:L].cpu().numpy().view(np.uint32)) == it["final_sha256"], kw
 
 
-@pytest.mark.parametrize("run_idx,n_s", [(0, None), (3, 600)])
-def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
-    """The GPU leg of the pair-seed pipeline (SA_ClientAgent.py:256-292), every pair of every
-    client in every iteration of run 0: public keys b_j G and the ECDH points a_i (b_j G) by the
-    batched flm_ec_mul the protocol uses (protocol._ecdh_batch), r_ij = SHA-256 of the point on
-    the GPU (flm_ec_combine with no shares: point = c1, seed = SHA-256(c1)), h_ijt from
-    ChaCha20 on the GPU (and by the client agent's batched pair_prf), hash-to-curve on the host, s_ij = SHA-256 on the GPU -- against the
-    r_ij and s_ij the reference's clients derived from refshim's deterministic pki keys.
-    Run D (N = 1024, -o 2: 40k pairs) checks every r_ij and h_ijt, and s_ij on its first n_s
-    pairs (hash-to-curve is host Python)."""
+@pytest.mark.parametrize("run_idx", [0, 3])
+def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx):
+    """The whole pair-seed pipeline (SA_ClientAgent.py:256-292) on the GPU, every pair of every
+    client in every iteration: public keys b_j G and the ECDH points a_i (b_j G) by the batched
+    flm_ec_mul the protocol uses (protocol._ecdh_batch), r_ij = SHA-256 of the point
+    (flm_ec_combine with no shares: point = c1, seed = SHA-256(c1)), h_ijt from ChaCha20 (and by
+    the client agent's batched pair_prf), H = hash-to-curve from the one-launch table of all 2^16
+    h values (flm_hash_to_curve_decimal), s_ij = SHA-256(H) -- against the r_ij, h_ijt, H and s_ij
+    the reference's clients derived from refshim's deterministic pki keys.  Run D is N = 1024,
+    -o 2: ~40k pairs per iteration."""
     from flamingo_amd import crypto as C
+    from flamingo_amd.abides.flamingo.client_agent import pair_prf
     from refgold import key_scalar
     run = ref["runs"][run_idx]
     N = run["N"]
@@ -129,6 +130,8 @@ def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
     g = np.tile(np.frombuffer(C.point_bytes(C.G), np.uint8), (N, 1))
     pub, fl = eng.ec_mul_wire(g, C.scalars_to_wire(keys))               # A_j = b_j G, on the GPU
     assert not fl.any()
+    table, tfl = eng.hash_to_curve_decimal(0, 1 << 16)
+    assert not tfl.any()
     none_sh, none_l = np.zeros((0, 1, 64), np.uint8), np.zeros((0, 32), np.uint8)
     for it in run["iterations"]:
         pre = f"{run['name']}_it{it['iteration']}_"
@@ -137,16 +140,15 @@ def test_gpu_ecdh_pair_seeds_match_reference(eng, ref, refnpz, run_idx, n_s):
         assert not fl.any()
         _, r, _ = eng.ec_combine_wire(pts, none_sh.reshape(0, len(pairs), 64), none_l, negate=False)
         assert np.array_equal(r, refnpz[pre + "r"]), it["iteration"]
-        hs = [str(int.from_bytes(eng.chacha20_encrypt(bytes(x), it["iteration"].to_bytes(16, "big"))[:4], "big")
-                  & 0xFFFF) for x in r]
+        hs = pair_prf(eng, [bytes(x) for x in r], it["iteration"])      # PRG word 0 of every r_ij, one launch
         assert hs == [h for c in it["clients"] for h in c["h"]]
-        # the client agent's own batched form: PRG word 0 of every r_ij in one launch
-        from flamingo_amd.abides.flamingo.client_agent import pair_prf
-        assert pair_prf(eng, [bytes(x) for x in r], it["iteration"]) == hs
-        n = len(hs) if n_s is None else min(n_s, len(hs))
-        H = np.stack([np.frombuffer(C.point_bytes(C.hash_str_to_curve(h)), np.uint8) for h in hs[:n]])
-        _, s, _ = eng.ec_combine_wire(H, none_sh.reshape(0, n, 64), none_l, negate=False)
-        assert np.array_equal(s, refnpz[pre + "s"][:n]), it["iteration"]
+        if run_idx == 0:                                                 # the per-key ChaCha20 form too
+            assert hs == [str(int.from_bytes(eng.chacha20_encrypt(bytes(x), it["iteration"].to_bytes(16, "big"))[:4],
+                                             "big") & 0xFFFF) for x in r]
+        H = table[np.array([int(h) for h in hs])]
+        assert np.array_equal(H, refnpz[pre + "h2c_point"]), it["iteration"]
+        _, s, _ = eng.ec_combine_wire(H, none_sh.reshape(0, len(hs), 64), none_l, negate=False)
+        assert np.array_equal(s, refnpz[pre + "s"]), it["iteration"]
 
 
 def test_device_resident_server_matches_reference(eng, ref, refnpz):

@@ -100,6 +100,6 @@ if backend == "nccl":
     okt = okt.to(dev)
 dist.all_reduce(okt, op=dist.ReduceOp.MIN)
 print(f"sharded reconstruction ok={bool(okt.item())}", flush=True)
-dist.destroy_process_group()
-eng.close()
+from flamingo_amd.distributed import shutdown  # noqa: E402
+shutdown(eng)                   # library communicator, then torch's process group, then the context
 sys.exit(0 if okt.item() else 1)

@@ -64,12 +64,15 @@ for step in "$@"; do
       AMD_LOG_LEVEL=4 timeout -k 10 300 python -u tools/rccl_clique_smoke.py gloo > "$O/${TAG}_rccl_amdlog.out" \
         2> "$O/${TAG}_rccl_amdlog.err" || { tail -20 "$O/${TAG}_rccl_amdlog.out"; exit 1; }
       python tools/kernel_log_summary.py "$O/${TAG}_rccl_amdlog.err" "$O/${TAG}_rccl_kernels.json" && rm -f "$O/${TAG}_rccl_amdlog.err" ;;
-    rccltrace)
-      # rocprofv3 kernel trace of the same script (last step of a call: with RCCL loaded the
-      # profiled process has crashed in its exit-time destructors, after every check passed)
-      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$O/${TAG}_rccl_trace" -o run -- python3 "$R/tools/rccl_clique_smoke.py" gloo > "$O/${TAG}_rccl_trace.log" 2>&1) \
-        || { tail -20 "$O/${TAG}_rccl_trace.log"; exit 1; } ;;
+    rccltrace|rccltrace:*)
+      # rocprofv3 kernel trace of the same script with torch's process group on backend ${step#rccltrace:}
+      # (default nccl: torch's ProcessGroupNCCL beside the library communicator, torn down in the order
+      # of distributed.shutdown); /proc/self/maps at interpreter exit goes next to the log
+      be=nccl; [ "$step" != rccltrace ] && be=${step#rccltrace:}
+      (cd /tmp && FLM_EXIT_MAPS="$O/${TAG}_rccl_trace_${be}.maps" timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+        --output-format csv -d "$O/${TAG}_rccl_trace_${be}" -o run -- python3 "$R/tools/rccl_clique_smoke.py" "$be" \
+        > "$O/${TAG}_rccl_trace_${be}.log" 2>&1) || { tail -40 "$O/${TAG}_rccl_trace_${be}.log"; exit 1; }
+      tail -3 "$O/${TAG}_rccl_trace_${be}.log" ;;
     ecpmc:*)
       # one PMC pass over tools/ec_bench.py (the combine, T = 20, Lagrange scalars) with ec_coop ${step#ecpmc:}
       (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \

@@ -77,6 +77,6 @@ for comm in ("torch", "rccl"):
                 print(f"{comm} non-current stream rep {rep} round {i + 1}: out==want {e}", flush=True)
                 ok &= e
 print(f"rccl async pipelined rounds ok={ok}", flush=True)
-dist.destroy_process_group()
-eng.close()
+from flamingo_amd.distributed import shutdown  # noqa: E402
+shutdown(eng)                   # library communicator, then torch's process group, then the context
 sys.exit(0 if ok else 1)

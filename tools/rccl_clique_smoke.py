@@ -9,9 +9,10 @@ under rocprofv3 is the evidence that they execute; tools/gpu.sh step `rccl`).
   ShardedReconstruction's flm_all_gather_dev + flm_reduce_scatter_dev.
 Every result is checked against the C oracle or the |U| invariant; exits non-zero on a mismatch.
 Argument: the torch.distributed backend of the world-1 group (nccl, default, or gloo).  The
-collectives under test are the library's own RCCL communicator either way; gloo keeps torch's
-ProcessGroupNCCL out of the process, which the rocprofv3 trace of this script needs (under the
-profiler that process group's teardown crashed at exit, after every check had passed)."""
+collectives under test are the library's own RCCL communicator either way.  Teardown is
+distributed.shutdown: library communicator (finalize + destroy) before torch's process group --
+the round-4 order (torch's group first) crashed at exit under rocprofv3 with the nccl backend.
+FLM_EXIT_MAPS=path saves /proc/self/maps at interpreter exit (to attribute any exit-time crash)."""
 import os
 import sys
 
@@ -32,6 +33,13 @@ from flamingo_amd.ingest import VectorStore  # noqa: E402
 from flamingo_amd.synthetic import recovery_round  # noqa: E402
 
 ok = True
+
+if os.environ.get("FLM_EXIT_MAPS"):
+    # the process's mappings just before the C-level exit handlers run, so that the frames of a
+    # crash in __cxa_finalize (the round-4 failure mode) can be attributed to a library
+    import atexit
+    import shutil
+    atexit.register(lambda: shutil.copyfile("/proc/self/maps", os.environ["FLM_EXIT_MAPS"]))
 
 
 def check(name, good):
@@ -130,7 +138,7 @@ rec.run_from_partial(S_shard, t(R["lambdas"]), t(R["mi_shares"]), t(R["c1"][a:b]
                      t(R["pair_signs"]), D, out)
 torch.cuda.synchronize()
 check("ShardedReconstruction report + run_from_partial", bool(torch.all(out[:L] == len(on)).item()))
-dist.destroy_process_group()
-eng.close()
+from flamingo_amd.distributed import shutdown  # noqa: E402
+shutdown(eng)                   # library communicator, then torch's process group, then the context
 print(f"rccl clique smoke ok={ok}", flush=True)
 sys.exit(0 if ok else 1)
