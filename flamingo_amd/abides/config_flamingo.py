@@ -7,7 +7,11 @@ construction (:179-215), cubic latency model (:225-238) and result print
 (:253-266).  Extra flags: --vector_len (reference constant 16000,
 util/param.py:8), --root_seed_hex (the reference draws it at random,
 util/param.py:31), --offline id,id,... (clients that crash before sending in
-every iteration: explicit dropout injection).
+every iteration: explicit dropout injection), --dropout F (in each iteration t a
+fresh offline set PCG64(seed=t).choice(N, round(F N), replace=False), SURVEY 8d's
+c5 recipe: BASELINE c5 is -n 4096 --vector_len 1048576 -i 10 --dropout 0.01).
+At the end the run prints, per iteration, |U| and whether final_sum == |U| in
+every slot (the all-ones known answer, SA_ClientAgent.py:304 + SA_ServiceAgent.py:605).
 """
 from __future__ import annotations
 
@@ -45,9 +49,22 @@ def parse(argv):
     ap.add_argument("--vector_len", type=int, default=P.vector_len)
     ap.add_argument("--root_seed_hex", default=None)
     ap.add_argument("--offline", default="")
+    ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--committee_size", type=int, default=P.committee_size)
     args, _ = ap.parse_known_args(argv)
     return ap, args
+
+
+def offline_schedule(n: int, iterations: int, always=(), dropout: float = 0.0) -> dict:
+    """client id -> iterations in which it crashes before sending: `always` in every iteration, plus
+    a fresh PCG64(seed=t).choice(n, round(dropout n), replace=False) set in each iteration t."""
+    out = {i: set(range(1, iterations + 1)) for i in always}
+    k = int(round(dropout * n))
+    for t in range(1, iterations + 1):
+        if k:
+            for i in np.random.Generator(np.random.PCG64(t)).choice(n, k, replace=False):
+                out.setdefault(int(i), set()).add(t)
+    return out
 
 
 def run(argv=None):
@@ -66,6 +83,7 @@ def run(argv=None):
         raise ValueError("committee_size cannot exceed num_clients")
     param.configure(root=root, L=args.vector_len, committee=args.committee_size)
     offline = {int(x) for x in args.offline.split(",") if x.strip()}
+    offline_its = offline_schedule(n, args.num_iterations, offline, args.dropout)
     print(f"Silent mode: {log.silent_mode}")
     print(f"Configuration seed: {seed}\n")
 
@@ -82,7 +100,7 @@ def run(argv=None):
             id=i, name=f"PPFL Client Agent {i}", type="ClientAgent", iterations=args.num_iterations, num_clients=n,
             neighborhood_size=args.neighborhood_size, debug_mode=args.debug_mode,
             random_state=np.random.RandomState(seed=np.random.randint(low=0, high=2**32, dtype="uint64")),
-            offline_iterations=range(1, args.num_iterations + 1) if i in offline else ()))
+            offline_iterations=offline_its.get(i, ())))
     print(f"Client init took {timedelta(seconds=time() - t0)}")
     server = ServiceAgent(
         id=n, name="PPFL Service Agent", type="ServiceAgent",
@@ -111,6 +129,14 @@ def run(argv=None):
     print(f"    Report step:         {results['clt_report'] / n}")
     print(f"    Crosscheck step:     {results['clt_crosscheck'] / param.committee_size}")
     print(f"    Reconstruction step: {results['clt_reconstruction'] / param.committee_size}")
+    print()
+    print("######## Known answer (all-ones inputs: final_sum == |U| in every slot) ########")
+    for it in sorted(server.results):
+        out, u = server.results[it], server.online_counts[it]
+        gpu = server.gpu_ms.get(it, {})
+        print(f"    iteration {it}: |U| = {u}, dropout pairs = {server.pairs_per_iteration.get(it, 0)}, "
+              f"final_sum == |U| in every slot: {bool(np.all(out == u))}; report GPU {gpu.get('report', 0):.3f} ms, "
+              f"unmask + D2H {gpu.get('reconstruction_unmask_wall', 0):.3f} ms")
     print()
     results["server"] = server
     return results

@@ -76,6 +76,7 @@ class SA_ServiceAgent(Agent):
         self.current_round = 0
         self.results = {}            # iteration -> final_sum (kept for inspection / tests)
         self.online_counts = {}      # iteration -> |U|
+        self.pairs_per_iteration = {}  # iteration -> D dropout pairs recovered
         self.aggProcessingMap = {0: self.initialize, 1: self.report, 2: self.forward_signatures,
                                  3: self.reconstruction}
         self.namedict = {0: "initialize", 1: "report", 2: "forward_signatures", 3: "reconstruction"}
@@ -328,6 +329,7 @@ class SA_ServiceAgent(Agent):
         self.agent_print(f"reconstruction unmask: {len(seeds)} masks over S on the GPU(s) + D2H, {ms:.3f} ms")
         self.results[self.current_iteration] = self.final_sum
         self.online_counts[self.current_iteration] = len(self.user_vectors)
+        self.pairs_per_iteration[self.current_iteration] = len(self.recon_symbol)
         self.agent_print("final sum:", self.final_sum)
 
     # ----------------------------------------------------------------- util

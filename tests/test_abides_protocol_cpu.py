@@ -195,3 +195,29 @@ def test_vec_sum_partial_follows_the_store(oracle_engine):
         srv.vec_sum_partial = np.zeros(64, np.uint32)
     srv.reconstruction_clear_pool()
     assert not srv.vec_sum_partial.any()
+
+
+def test_offline_schedule_per_iteration():
+    """--dropout F: a fresh PCG64(seed=t).choice(N, round(F N)) offline set per iteration."""
+    from flamingo_amd.abides.config_flamingo import offline_schedule
+    sch = offline_schedule(4096, 10, always={5}, dropout=0.01)
+    for t in range(1, 11):
+        off = sorted(i for i, its in sch.items() if t in its and i != 5)
+        want = sorted(int(x) for x in np.random.Generator(np.random.PCG64(t)).choice(4096, 41, replace=False) if x != 5)
+        assert off == want, t
+        assert t in sch[5]
+    assert offline_schedule(128, 3) == {}
+
+
+def test_protocol_per_iteration_dropouts_on_oracle(oracle_engine, capsys):
+    from flamingo_amd.abides.config_flamingo import offline_schedule, run
+    argv = ["-c", "flamingo", "-n", "32", "-i", "3", "-s", "9", "-k", "--vector_len", "512",
+            "--committee_size", "9", "--root_seed_hex", "22" * 32, "--round_time", "30", "--dropout", "0.1"]
+    srv = run(argv)["server"]
+    sch = offline_schedule(32, 3, dropout=0.1)
+    assert sorted(srv.results) == [1, 2, 3]
+    for it, out in srv.results.items():
+        n_off = sum(1 for its in sch.values() if it in its)
+        assert n_off == 3 and srv.online_counts[it] <= 32 - n_off
+        assert np.all(out == srv.online_counts[it]) and srv.pairs_per_iteration[it] > 0
+    assert "final_sum == |U| in every slot: True" in capsys.readouterr().out

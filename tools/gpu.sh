@@ -54,6 +54,22 @@ for step in "$@"; do
     sim)
       timeout -k 10 300 python -m flamingo_amd.abides -c flamingo -n 128 -i 1 -p 1 > "$O/${TAG}_sim_c1_n128.log" 2>&1 || exit 1
       timeout -k 10 600 python -m flamingo_amd.abides -c flamingo -n 1024 -i 2 -p 1 > "$O/${TAG}_sim_n1024_i2.log" 2>&1 || exit 1 ;;
+    simc5r)
+      # BASELINE c5's shape with L = 2^16 and 2 iterations (1 % per-iteration dropouts) through the agents
+      timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 65536 -i 2 --dropout 0.01 \
+        -k -s 5 > "$O/${TAG}_sim_c5r.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5r.log"; exit 1; }
+      tail -12 "$O/${TAG}_sim_c5r.log" ;;
+    simc3)
+      # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
+      timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \
+        > "$O/${TAG}_sim_c3.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c3.log"; exit 1; }
+      tail -12 "$O/${TAG}_sim_c3.log" ;;
+    simc5)
+      # BASELINE c5 through the agents: n = 4096, L = 2^20, 10 iterations, 1 % per-iteration dropouts;
+      # FLM_GPUS=all: the server's steps over every visible GPU (one here, all 8 on the 8-GPU node)
+      FLM_GPUS=all timeout -k 10 1100 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 10 \
+        --dropout 0.01 -k -s 5 > "$O/${TAG}_sim_c5.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5.log"; exit 1; }
+      tail -24 "$O/${TAG}_sim_c5.log" ;;
     rccl)
       # every RCCL branch of the multi-GPU path on the one GPU (tools/rccl_clique_smoke.py), then the
       # same script under a kernel + memory-copy trace: the RCCL kernels / copies it launched
@@ -73,6 +89,11 @@ for step in "$@"; do
         --output-format csv -d "$O/${TAG}_rccl_trace_${be}" -o run -- python3 "$R/tools/rccl_clique_smoke.py" "$be" \
         > "$O/${TAG}_rccl_trace_${be}.log" 2>&1) || { tail -40 "$O/${TAG}_rccl_trace_${be}.log"; exit 1; }
       tail -3 "$O/${TAG}_rccl_trace_${be}.log" ;;
+    h2c)
+      # the hash-to-curve table launch under a kernel trace (tools/h2c_bench.py)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${TAG}_h2c" -o run \
+        -- python3 "$R/tools/h2c_bench.py" > "$O/${TAG}_h2c.log" 2>&1) || { tail -20 "$O/${TAG}_h2c.log"; exit 1; }
+      grep '^{' "$O/${TAG}_h2c.log" | cut -c1-600 ;;
     ecpmc:*)
       # one PMC pass over tools/ec_bench.py (the combine, T = 20, Lagrange scalars) with ec_coop ${step#ecpmc:}
       (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \
