@@ -9,7 +9,10 @@ util/param.py:8), --root_seed_hex (the reference draws it at random,
 util/param.py:31), --offline id,id,... (clients that crash before sending in
 every iteration: explicit dropout injection), --dropout F (in each iteration t a
 fresh offline set PCG64(seed=t).choice(N, round(F N), replace=False), SURVEY 8d's
-c5 recipe: BASELINE c5 is -n 4096 --vector_len 1048576 -i 10 --dropout 0.01).
+c5 recipe: BASELINE c5 is -n 4096 --vector_len 1048576 -i 10 --dropout 0.01),
+--latency deterministic (model/LatencyModel.py:142-143: min latency only, so no
+VECTOR arrives late and the offline sets are exactly the injected ones; the
+reference config's cubic model, the default, adds emergent late-message dropouts).
 At the end the run prints, per iteration, |U| and whether final_sum == |U| in
 every slot (the all-ones known answer, SA_ClientAgent.py:304 + SA_ServiceAgent.py:605).
 """
@@ -50,6 +53,7 @@ def parse(argv):
     ap.add_argument("--root_seed_hex", default=None)
     ap.add_argument("--offline", default="")
     ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--latency", choices=("cubic", "deterministic"), default="cubic")
     ap.add_argument("--committee_size", type=int, default=P.committee_size)
     args, _ = ap.parse_known_args(argv)
     return ap, args
@@ -113,7 +117,7 @@ def run(argv=None):
     model_args = {"connected": True,
                   "min_latency": np.random.uniform(low=10000000, high=100000000, size=pairwise),
                   "jitter": 0.3, "jitter_clip": 0.05, "jitter_unit": 5}
-    latency = LatencyModel(latency_model="cubic", random_state=latency_rstate, kwargs=model_args)
+    latency = LatencyModel(latency_model=args.latency, random_state=latency_rstate, kwargs=model_args)
     results = kernel.runner(agents=agents, startTime=start, stopTime=stop, agentLatencyModel=latency,
                             defaultComputationDelay=default_delay, skip_log=args.skip_log, log_dir=args.log_dir)
     print()

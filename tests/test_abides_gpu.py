@@ -69,3 +69,43 @@ def test_simulation_on_a_device_group(monkeypatch, spec):
     srv._store.close()                      # the group refuses to close under a live store
     grp.close()
     protocol._group = None
+
+
+def test_simulation_c5_shape_reduced():
+    """BASELINE c5's client count and per-iteration 1 % dropouts (--dropout 0.01: PCG64(seed=t)
+    choice per iteration) through the agents, with L = 2^16 and 2 iterations; deterministic latency,
+    so the offline sets are exactly the injected ones (41 per iteration)."""
+    from flamingo_amd.abides.config_flamingo import offline_schedule, run
+    res = run(["-c", "flamingo", "-n", "4096", "--vector_len", "65536", "-i", "2", "--dropout", "0.01", "-k",
+               "-s", "5", "--latency", "deterministic"])
+    srv = res["server"]
+    sch = offline_schedule(4096, 2, dropout=0.01)
+    assert sorted(srv.results) == [1, 2]
+    for it, out in srv.results.items():
+        assert srv.online_counts[it] == 4096 - sum(1 for its in sch.values() if it in its) == 4055
+        assert np.all(out == 4055), it
+        assert srv.pairs_per_iteration[it] > 500
+
+
+def test_assigned_vec_sum_partial_on_the_gpu():
+    """ADVICE r4 (medium), with the GPU engine: an assigned vec_sum_partial is what the masks are
+    added to when reconstruction_process runs without a report (SA_ServiceAgent.py:540/605)."""
+    import oracle as O
+    from flamingo_amd.abides.flamingo import protocol
+    from flamingo_amd.abides.flamingo.service_agent import SA_ServiceAgent
+    protocol.configure(L=4096)
+    try:
+        srv = SA_ServiceAgent(0, "srv", "SA_ServiceAgent", random_state=np.random.RandomState(1), num_clients=4,
+                              users={1, 2, 3})
+        base = np.random.default_rng(4).integers(0, 2**32, 4096, dtype=np.uint32)
+        srv.vec_sum_partial = base
+        m = 0xDEADBEEF12345
+        srv.committee_threshold = 1
+        srv.committee_shares_mi, srv.recon_index = {7: [m]}, {7: 1}
+        srv.dec_target_pairwise, srv.recon_symbol = {}, {}
+        srv.reconstruction_process()
+        want = O.aggregate_unmask(base[None], np.frombuffer(m.to_bytes(32, "big"), np.uint8)[None],
+                                  np.array([-1], np.int8), L=4096)
+        assert np.array_equal(srv.final_sum, want)
+    finally:
+        protocol.configure(committee=60)

@@ -56,7 +56,7 @@ for step in "$@"; do
       timeout -k 10 600 python -m flamingo_amd.abides -c flamingo -n 1024 -i 2 -p 1 > "$O/${TAG}_sim_n1024_i2.log" 2>&1 || exit 1 ;;
     simc5r)
       # BASELINE c5's shape with L = 2^16 and 2 iterations (1 % per-iteration dropouts) through the agents
-      timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 65536 -i 2 --dropout 0.01 \
+      timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 65536 -i 2 --dropout 0.01 --latency deterministic \
         -k -s 5 > "$O/${TAG}_sim_c5r.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5r.log"; exit 1; }
       tail -12 "$O/${TAG}_sim_c5r.log" ;;
     simc3)
@@ -68,7 +68,7 @@ for step in "$@"; do
       # BASELINE c5 through the agents: n = 4096, L = 2^20, 10 iterations, 1 % per-iteration dropouts;
       # FLM_GPUS=all: the server's steps over every visible GPU (one here, all 8 on the 8-GPU node)
       FLM_GPUS=all timeout -k 10 1100 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 10 \
-        --dropout 0.01 -k -s 5 > "$O/${TAG}_sim_c5.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5.log"; exit 1; }
+        --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_sim_c5.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5.log"; exit 1; }
       tail -24 "$O/${TAG}_sim_c5.log" ;;
     rccl)
       # every RCCL branch of the multi-GPU path on the one GPU (tools/rccl_clique_smoke.py), then the
