@@ -36,3 +36,13 @@ def test_model_predicts_the_threshold():
     p = M.predict(M.check(n_random=300, seed=7))
     assert p["dbl_chain_instr"][1] < 0.6 * p["dbl_chain_instr"][0]
     assert p["saving"] >= 0.20
+
+
+def test_interleave_model_predicts_no_gain():
+    """two products interleaved per row against the measured row kernel.  The
+    SIMD already issues its waves into each other's DPP latency, so within-wave interleave cannot beat
+    spreading the same products over waves; below the 20 % bar everywhere (not built)."""
+    import ec_row_model as R
+    for name, r in R.interleave_report():
+        assert r["saving"] < 0.2, name
+    assert R.interleave_model(2420, 256)["cycles_per_step_now"] > R.LONE_CPI      # D = 121 is issue-bound

@@ -161,6 +161,49 @@ def predict(hist, dbl_us=2.36, add_us=8.65, n_dbl=258, n_add=50, finish_ms=0.15,
             "saving": 1 - row_ms / lane_ms}
 
 
+# ---------------------------------------------------------------- interleave model
+# Measured (DESIGN.md sections 5 and 10.2, profiles/r04_ec_kernel_sweep.log, r04_rank8_row.log):
+LONE_MUL_NS = 279.0          # one row-field multiplication, one wave alone on its SIMD: 93 instructions
+LONE_CPI = 6.5               # cycles per instruction of that lone chain (the DPP read waits on the last mad)
+DBL_US_LONE = 1.78           # one doubling, lone wave
+DBL_US_D120 = 2.38           # one doubling in the whole-GPU combine at D = 120, T = 20 (2,400 products)
+ADD_US_LONE, ADD_US_D120 = 2.4, 3.2
+SIMDS = 256 * 4
+
+
+def interleave_model(products=2400, cus=256, k=2):
+    """Cycles per formula step (one dependent instruction of every chain) on the busiest SIMD of the
+    row kernel, now (one product per wave) and with k independent products interleaved per wave.
+
+    A SIMD holding n waves, each a dependent chain, issues one instruction of each per step and takes
+    max(L, n c) cycles for it: L = the lone chain's cycles per instruction (the DPP reads wait on the
+    previous v_mad_u64_u32), c = the SIMD's issue cost of one wave instruction.  The busiest SIMD holds
+    ceil(products / SIMDs) waves today, ceil(products / (k SIMDs)) waves of k instructions per step
+    interleaved.  c is calibrated on the D = 120 measurement: 2,400 products on 1,024 SIMDs (3 waves
+    on the busiest), 2.38 us per doubling against 1.78 us for a lone wave."""
+    import math
+    simds = cus * 4
+    c = DBL_US_D120 / DBL_US_LONE * LONE_CPI / math.ceil(2400 / SIMDS)
+    n_now = math.ceil(products / simds)
+    n_int = math.ceil(products / (k * simds))
+    now = max(LONE_CPI, n_now * c)
+    inter = max(LONE_CPI, n_int * k * c)
+    return {"busiest_simd_waves_now": n_now, "busiest_simd_waves_interleaved": n_int,
+            "issue_cycles_per_instr": round(c, 3), "cycles_per_step_now": round(now, 3),
+            "cycles_per_step_interleaved": round(inter, 3), "saving": round(1 - inter / now, 4)}
+
+
+def interleave_report():
+    rows = []
+    for name, products, cus in (("whole-GPU combine, c5 one rank of G = 8 (D = 121 x T = 20)", 2420, 256),
+                                ("the same on the rank's 72 EC CUs (beside the self-mask pass)", 2420, 72),
+                                ("whole-GPU combine, c5 on one GPU (D = 962 x T = 20)", 19240, 256),
+                                ("a small batch on 8 CUs, one product per SIMD (32 products)", 32, 8),
+                                ("a small batch on 8 CUs, two products per SIMD (64 products)", 64, 8)):
+        rows.append((name, interleave_model(products, cus)))
+    return rows
+
+
 if __name__ == "__main__":
     h = check()
     for k, v in h.items():
@@ -172,3 +215,7 @@ if __name__ == "__main__":
     print("addition critical path (lane, row): %.0f, %.0f instructions" % p["add_chain_instr"])
     print("one G = 8 rank's combine (D = 120 x T = 20): per-lane model %.3f ms, row model %.3f ms: %.0f %% less"
           % (p["combine_ms_lane_model"], p["combine_ms_row_model"], 100 * p["saving"]))
+    print()
+    print("two products interleaved per row (k = 2), cycles per formula step on one SIMD:")
+    for name, r in interleave_report():
+        print(f"  {name}: {r}")
