@@ -42,7 +42,9 @@ for _name, _res, _args in (
         ("flm_store_add", _int, [_vp, ctypes.c_int64, _vp, _sz]),
         ("flm_store_partial", _int, [_vp]),
         ("flm_store_unmask", _int, [_vp, _u8p, _i8p, _int, _u32p]),
-        ("flm_store_reset", _int, [_vp])):
+        ("flm_store_reset", _int, [_vp]),
+        ("flm_hash_to_curve", _int, [_vp, _u8p, _u32p, _int, _u8p, _u32p]),
+        ("flm_hash_to_curve_decimal", _int, [_vp, ctypes.c_uint32, _int, _u8p, _u32p])):
     _f = getattr(_lib, _name)
     _f.restype, _f.argtypes = _res, _args
 
@@ -147,6 +149,46 @@ def ec_combine(c1_points, shares_by_member, coeffs):
     _check(_lib.flm_ec_combine(_context(), xy(c1_points).ctypes.data_as(_u8p), sh.ctypes.data_as(_u8p),
                                _be(coeffs).ctypes.data_as(_u8p), T, D, 1, None, seeds.ctypes.data_as(_u8p), None))
     return [seeds[32 * i:32 * i + 32].tobytes() for i in range(D)]
+
+
+class Point:
+    """The .x / .y of pycryptodome's EccPoint, which is all SA_ClientAgent.py:288-289 and the
+    ElGamal encryption (:434-447, via ECC.EccPoint(x, y)) read of a hash-to-curve result."""
+    __slots__ = ("x", "y")
+
+    def __init__(self, x, y):
+        self.x, self.y = x, y
+
+
+_h2c_table = None
+
+
+def hash_str_to_curve(msg):
+    """ecchash.hash_str_to_curve(msg, count=2, modulus=n, degree=1, blen=48, XMD SHA-256) as
+    SA_ClientAgent.py:283-286 calls it, on the GPU.  The client's h_ijt is str(x & 0xFFFF) (:280):
+    the first such call computes all 2^16 points in one launch (flm_hash_to_curve_decimal) and later
+    calls index the table; any other message (<= 64 bytes) is one flm_hash_to_curve launch."""
+    global _h2c_table
+    if isinstance(msg, str) and msg.isdigit() and str(int(msg)) == msg and int(msg) < (1 << 16):
+        if _h2c_table is None:
+            out = np.empty((1 << 16, 64), np.uint8)
+            fl = np.empty(1 << 16, np.uint32)
+            _check(_lib.flm_hash_to_curve_decimal(_context(), 0, 1 << 16, out.ctypes.data_as(_u8p),
+                                                  fl.ctypes.data_as(_u32p)))
+            _h2c_table = (out, fl)
+        row, f = _h2c_table[0][int(msg)], int(_h2c_table[1][int(msg)])
+    else:
+        m = msg.encode() if isinstance(msg, str) else bytes(msg)
+        buf = np.zeros(64, np.uint8)
+        buf[:len(m)] = np.frombuffer(m, np.uint8)
+        out, fl, ln = np.empty(64, np.uint8), np.zeros(1, np.uint32), np.array([len(m)], np.uint32)
+        _check(_lib.flm_hash_to_curve(_context(), buf.ctypes.data_as(_u8p), ln.ctypes.data_as(_u32p), 1,
+                                      out.ctypes.data_as(_u8p), fl.ctypes.data_as(_u32p)))
+        row, f = out, int(fl[0])
+    if f & 4:
+        return Point(0, 0)                   # the point at infinity, as pycryptodome's EccPoint(0, 0)
+    b = row.tobytes()
+    return Point(int.from_bytes(b[:32], "big"), int.from_bytes(b[32:], "big"))
 
 
 def client_mask(seeds, signs, L, x=None):

@@ -34,7 +34,8 @@ def test_binding_loads_and_binds(monkeypatch):
     flm = load_binding(monkeypatch)
     for name in ("flm_aggregate_unmask", "flm_client_mask", "flm_shamir_combine", "flm_ec_combine",
                  "flm_group_aggregate_unmask", "flm_store_create", "flm_store_add", "flm_store_partial",
-                 "flm_store_unmask", "flm_store_reset", "flm_store_free"):
+                 "flm_store_unmask", "flm_store_reset", "flm_store_free", "flm_hash_to_curve",
+                 "flm_hash_to_curve_decimal"):
         assert getattr(flm._lib, name).argtypes
 
 
@@ -102,3 +103,20 @@ def test_binding_reproduces_reference_round(monkeypatch, ref, refnpz):
         flm.aggregate_unmask([rows[0].astype(np.float32)], [], [], L)
     st.close()
     assert st.h is None
+
+
+@pytest.mark.gpu
+def test_binding_hash_to_curve_matches_reference(monkeypatch, ref, refnpz):
+    """The client edit at SA_ClientAgent.py:283-286: flm.hash_str_to_curve(h_ijt) gives the points the
+    reference's own ecchash produced in run A (.x / .y as the EccPoint it replaces)."""
+    flm = load_binding(monkeypatch)
+    run = ref["runs"][0]
+    it = run["iterations"][0]
+    pts = refnpz[f"{run['name']}_it{it['iteration']}_h2c_point"]
+    hs = [h for c in it["clients"] for h in c["h"]]
+    for k in range(0, len(hs), 7):
+        p = flm.hash_str_to_curve(hs[k])
+        assert p.x.to_bytes(32, "big") + p.y.to_bytes(32, "big") == bytes(pts[k])
+    import ec_oracle as E
+    q = flm.hash_str_to_curve("abcdeefekf")                 # the ecchash.py:303 demo message (not a table key)
+    assert (q.x, q.y) == E.hash_str_to_curve("abcdeefekf")

@@ -59,6 +59,14 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 65536 -i 2 --dropout 0.01 --latency deterministic \
         -k -s 5 > "$O/${TAG}_sim_c5r.log" 2>&1 || { tail -30 "$O/${TAG}_sim_c5r.log"; exit 1; }
       tail -12 "$O/${TAG}_sim_c5r.log" ;;
+    simprof)
+      # where the host time of the agent simulation goes: cProfile of the reduced c5 run
+      timeout -k 10 900 python -u -m cProfile -o "$O/${TAG}_sim_c5r.prof" -m flamingo_amd.abides -c flamingo -n 4096 \
+        --vector_len 65536 -i 2 --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_sim_c5r_prof.log" 2>&1 \
+        || { tail -30 "$O/${TAG}_sim_c5r_prof.log"; exit 1; }
+      python -c "import pstats,sys; p=pstats.Stats(sys.argv[1]); p.sort_stats('tottime').print_stats(40); p.sort_stats('cumulative').print_stats(60)" \
+        "$O/${TAG}_sim_c5r.prof" > "$O/${TAG}_sim_c5r_pstats.txt" 2>&1
+      head -70 "$O/${TAG}_sim_c5r_pstats.txt" | tail -50 ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \
