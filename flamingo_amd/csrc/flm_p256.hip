@@ -1563,6 +1563,125 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_kernel(const uint8
         }
     }
 }
+
+// ec_mul_row_kernel with Straus grouping: each 16-lane row sums NT consecutive terms of one pair,
+// sum_u lambda_{jg NT + u} share_{jg NT + u, i}, along ONE chain of doublings (NT tables of odd
+// multiples in LDS, NT digit strings).  Beside the self-mask pass the combine is issue-bound, so
+// what counts is the work per term: (258 / NT + 1) doublings + 50 additions instead of 259 + 50
+// (tools/ec_row_model.py straus_row_model: one G = 8 rank of c5 1.43 -> 1.19 / 1.07 ms predicted at
+// NT = 2 / 4; the chain itself grows to 0.70 / 0.95 ms).  Output: the per-row partial sums as planes
+// [ceil(T / NT)][24][D] for ec_finish_kernel, as ec_mul_straus_kernel.  Terms past T and off-curve
+// points enter as infinity (the latter with flag bit 1).
+template <int NT>
+__global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_straus_kernel(const uint8_t *__restrict__ points,
+                                                                         const uint8_t *__restrict__ scalars, int T,
+                                                                         int D, uint32_t *__restrict__ jac,
+                                                                         uint32_t *__restrict__ flags) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ uint32_t S[kCoopSlots * 64];
+    __shared__ uint32_t tab[NT][9 * 3 * 64];
+    const int lane = threadIdx.x & 63, r = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    RowField f;
+    f.K = row::make_ctx();
+    const int Tg = (T + NT - 1) / NT;
+    const size_t g = (size_t)blockIdx.x * 4 + (lane >> 4);
+    const bool valid = g < (size_t)Tg * D;
+    const int jg = valid ? (int)(g / D) : 0;
+    const int i = valid ? (int)(g - (size_t)jg * D) : 0;
+    int8_t dig[NT][kNafLen];
+#pragma unroll 1
+    for (int u = 0; u < NT; ++u) {
+        const int j = jg * NT + u;
+        const bool has = valid && j < T;
+        uint32_t x = 0, y = 0;
+        if (has && r < 8) {
+            const uint32_t *pw = reinterpret_cast<const uint32_t *>(points + ((size_t)j * D + i) * 64);
+            x = __builtin_bswap32(pw[7 - r]);
+            y = __builtin_bswap32(pw[15 - r]);
+        }
+        const uint32_t rhs = f.add(f.sub(f.mul(f.sqr(x), x), f.add(f.add(x, x), x)), r < 8 ? kBn[r & 7] : 0u);
+        const bool in_x = row::row_all8(row::canon(x, f.K) == x, f.K);
+        const bool in_y = row::row_all8(row::canon(y, f.K) == y, f.K);
+        const bool on_c = row::row_all8(row::canon(f.sqr(y), f.K) == row::canon(rhs, f.K), f.K);
+        const bool ok = has && in_x && in_y && on_c;
+        if (w == 0 && has && !ok && r == 0) atomicOr(&flags[i], 2u);
+        JacWT<uint32_t> PW;
+        PW.X = ok ? x : f.one();
+        PW.Y = ok ? y : f.one();
+        PW.Z = ok ? f.one() : 0u;
+        PW.W = PW.Z;
+        if (has) {
+            wnaf5(scalars + (size_t)j * 32, dig[u]);
+        } else {
+#pragma unroll 1
+            for (int k = 0; k < kNafLen; ++k) dig[u][k] = 0;
+        }
+        uint32_t *tu = tab[u];
+        JacWT<uint32_t> P2 = PW;
+        coop_dbl_w(P2, w, lane, S, f);
+        if (w == 0) {
+            tu[0 * 64 + lane] = PW.X;
+            tu[1 * 64 + lane] = PW.Y;
+            tu[2 * 64 + lane] = PW.Z;
+            tu[3 * 64 + lane] = P2.X;
+            tu[4 * 64 + lane] = P2.Y;
+            tu[5 * 64 + lane] = P2.Z;
+        }
+        __syncthreads();
+        JacWT<uint32_t> t = PW;
+#pragma unroll 1
+        for (int k = 1; k < 8; ++k) {
+            coop_add_w(t, true, 1, false, w, lane, S, tu, f);
+            if (w == 0) {
+                uint32_t *q = tu + (size_t)(k == 1 ? 8 : k) * 3 * 64;
+                q[lane] = t.X;
+                q[64 + lane] = t.Y;
+                q[128 + lane] = t.Z;
+            }
+            __syncthreads();
+        }
+        if (w == 0) {
+            const uint32_t *q = tu + (size_t)8 * 3 * 64;
+            tu[3 * 64 + lane] = q[lane];
+            tu[4 * 64 + lane] = q[64 + lane];
+            tu[5 * 64 + lane] = q[128 + lane];
+        }
+        __syncthreads();
+    }
+    JacWT<uint32_t> acc;
+    acc.X = acc.Y = f.one();
+    acc.Z = acc.W = 0u;
+    int vn[NT];
+#pragma unroll
+    for (int u = 0; u < NT; ++u) vn[u] = dig[u][kNafLen - 1];  // one step ahead, as ec_mul_row_kernel
+#pragma unroll 1
+    for (int k = kNafLen - 1; k >= 0; --k) {
+        int v[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+            v[u] = vn[u];
+            if (k > 0) vn[u] = dig[u][k - 1];
+        }
+        coop_dbl_w(acc, w, lane, S, f);
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+            if (__any(v[u] != 0))
+                coop_add_w(acc, v[u] != 0, (v[u] < 0 ? -v[u] : v[u]) >> 1, v[u] < 0, w, lane, S, tab[u], f);
+    }
+    if (w == 0) {
+        const uint32_t rm = r < 8 ? kOne[r & 7] : 0u;
+        const uint32_t X = row::canon(f.mul(acc.X, rm), f.K);
+        const uint32_t Y = row::canon(f.mul(acc.Y, rm), f.K);
+        const uint32_t Z = row::canon(f.mul(acc.Z, rm), f.K);
+        if (valid && r < 8) {
+            uint32_t *o = jac + (size_t)jg * 24 * D + i;
+            o[(size_t)r * D] = X;
+            o[(size_t)(8 + r) * D] = Y;
+            o[(size_t)(16 + r) * D] = Z;
+        }
+    }
+}
 #endif  // FLM_COOP_MODJ
 
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
@@ -1976,6 +2095,21 @@ hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int 
                          uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop,
                          int terms, unsigned lds_pad) {
     if (T <= 0 || D <= 0) return hipSuccess;
+#if FLM_COOP_MODJ
+    if (coop == 2 && terms > 1 && !per_element) {  // row field, Straus: terms per row chain
+        const size_t n = (size_t)ec_mul_groups(T, terms) * D;
+        const dim3 grid((unsigned)((n + 3) / 4)), block(64 * kCoopWaves);
+        if (terms == 2)
+            hipLaunchKernelGGL(ec_mul_row_straus_kernel<2>, grid, block, 0, stream, d_points, d_scalars, T, D, d_jac,
+                               d_flags);
+        else if (terms == 4)
+            hipLaunchKernelGGL(ec_mul_row_straus_kernel<4>, grid, block, 0, stream, d_points, d_scalars, T, D, d_jac,
+                               d_flags);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+#endif
     if (terms > 1 && !per_element) {
         const size_t n = (size_t)ec_mul_groups(T, terms) * D;
         const dim3 grid((unsigned)((n + kEcThreads - 1) / kEcThreads));

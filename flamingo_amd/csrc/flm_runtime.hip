@@ -127,6 +127,7 @@ struct flm_ctx {
     int tune_ec_spread = 0;     // KiB of LDS reserved per 64-lane EC workgroup (0 = none): caps EC waves per CU
                                 // so a CU-masked dispatch spreads them one per SIMD instead of packing two
     int tune_ec_terms = 1;      // combine terms per lane (1, 2, 4: Straus, shared doublings)
+    int tune_ec_row_terms = 1;  // combine terms per row chain of the row-field kernel (1, 2, 4: Straus)
     int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 2: four
                                 // waves per 4, each element on a 16-lane row (ec_mul_row_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
@@ -1242,6 +1243,9 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "ec_terms") {
         if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_terms must be 1, 2 or 4");
         ctx->tune_ec_terms = value;
+    } else if (k == "ec_row_terms") {
+        if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_row_terms must be 1, 2 or 4");
+        ctx->tune_ec_row_terms = value;
     } else if (k == "ec_coop") {
         if (value < -1 || value > 2) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0, 1 or 2");
         ctx->tune_ec_coop = value;
@@ -1310,9 +1314,10 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_ON_DEVICE(ctx);
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
-    const int terms = ec_coop(ctx, (size_t)T * D) ? 1 : ctx->tune_ec_terms;
+    const int coop = ec_coop(ctx, (size_t)T * D);
+    const int terms = coop == 2 ? ctx->tune_ec_row_terms : (coop ? 1 : ctx->tune_ec_terms);
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
-                                    ctx->tune_ec_threads, ctx->tune_ec_waves, ec_coop(ctx, (size_t)T * D), terms,
+                                    ctx->tune_ec_threads, ctx->tune_ec_waves, coop, terms,
                                     1024u * (unsigned)ctx->tune_ec_spread));
     FLM_HIP(ctx, flm::launch_ec_finish(d_c1, ctx->ec_jac.as<uint32_t>(), flm::ec_mul_groups(T, terms), D, negate,
                                        d_points_out, d_seeds_out,

@@ -119,7 +119,8 @@ class MaskEngine:
 
     # flm_set_tuning defaults (include/flamingo_hip.h), for get_tuning before any set_tuning
     TUNING_DEFAULTS = {"variant": -1, "subtiles": 0, "pairing": 1, "min_items": 1024, "ec_threads": 64,
-                       "ec_waves": 1, "ec_coop": -1, "ec_terms": 1, "ec_spread": 0, "small": 1}
+                       "ec_waves": 1, "ec_coop": -1, "ec_terms": 1, "ec_row_terms": 1, "ec_spread": 0,
+                       "small": 1}
 
     def set_tuning(self, key: str, value: int):
         """A/B knobs: variant (-1 auto, 0..3) and subtiles (0 auto, 1, 4, 16)."""

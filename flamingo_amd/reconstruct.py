@@ -118,6 +118,8 @@ class ServerReconstruction:
         profiles/r03_recon_coop_confined_sweep.log), and `ec_terms` products per lane share one chain of
         doublings (Straus: 2 terms on 24 CUs 8.05 ms vs 1 term on 32 CUs 8.46, profiles/r02_straus_recon.log);
         unconfined, the library's auto choice stands."""
+        keys = ("ec_coop", "ec_terms", "ec_spread")
+        prev = {k: self.eng.get_tuning(k) for k in keys}
         if self.ec_cus > 0:
             self.eng.set_tuning("ec_coop", self.ec_coop)
             self.eng.set_tuning("ec_terms", self.ec_terms)
@@ -126,9 +128,8 @@ class ServerReconstruction:
             self.eng.ec_combine_dev(c1, pair_shares, lambdas, p_seeds, flags, stream=self.side)
         finally:
             if self.ec_cus > 0:
-                self.eng.set_tuning("ec_coop", -1)
-                self.eng.set_tuning("ec_terms", 1)
-                self.eng.set_tuning("ec_spread", 0)
+                for k in keys:                        # the caller's own settings, not the defaults
+                    self.eng.set_tuning(k, prev[k])
 
     def run(self, rows, L: int, lambdas, mi_shares, c1, pair_shares, pair_signs, out, stream=None,
             overlap: bool = True):

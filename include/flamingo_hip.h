@@ -176,6 +176,9 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
  *              (Straus: the terms share one chain of doublings); ignored when the combine
  *              runs cooperatively.
+ *   "ec_row_terms" 1 (default) | 2 | 4: the same Straus grouping inside the row-field cooperative
+ *              kernel (ec_coop 2): each 16-lane row sums that many terms of one pair along one
+ *              chain of doublings (less issue work per term, a longer chain).
  *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
  *              per-lane combine kernels (caps their workgroups per CU).
  *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev runs

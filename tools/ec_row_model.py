@@ -193,6 +193,37 @@ def interleave_model(products=2400, cus=256, k=2):
             "cycles_per_step_interleaved": round(inter, 3), "saving": round(1 - inter / now, 4)}
 
 
+# ---------------------------------------------------------------- Straus in the row kernel (round 5)
+# The issue-bound picture above, applied to one G = 8 rank's shares -> final: the combine's waves
+# (priority 3) and the self-mask pass share the SIMDs, so the rank's time is about the SUM of the two
+# issue workloads (bounded below by the combine's own chain latency).  Round 4 modelled Straus
+# grouping against the combine ALONE (latency-bound: -7 %); beside the pass it is the issue work that
+# counts.  Per-wave SIMD issue cost of one coop step, from the D = 120 calibration (3 waves on the
+# busiest SIMD): a doubling 2.38 / 3 us, an addition 3.2 / 3 us; lone-wave latency 1.78 / 2.4 us.
+DBL_ISSUE_US, ADD_ISSUE_US = DBL_US_D120 / 3, ADD_US_D120 / 3
+PASS_MS_G8 = 0.82          # one G = 8 rank's self-mask pass alone (K = 4,055 + 121 over 2^17 slots)
+RANK8_NOW_MS = (1.39, 1.52)  # measured: shares -> final, coop kernel on 72 CUs / row kernel unpartitioned
+
+
+def straus_row_model(g, D=121, T=20, simds=SIMDS, pass_ms=PASS_MS_G8, adds_per_term=50):
+    """g terms of one pair per row chain (a shared doubling chain, g tables of odd multiples):
+    chains = D ceil(T / g), each (258 + g) doublings (258 of the chain + one per table) and
+    g x 50 additions (43 wNAF + 7 table).  Returns the combine's issue work spread over the chip,
+    its lone chain latency, and the predicted shares -> final = max(latency, pass + work)."""
+    import math
+    chains = D * math.ceil(T / g)
+    dbl, add = 258 + g, adds_per_term * g
+    work_ms = chains * (dbl * DBL_ISSUE_US + add * ADD_ISSUE_US) / simds / 1e3
+    lat_ms = (dbl * DBL_US_LONE + add * ADD_US_LONE) / 1e3
+    return {"g": g, "chains": chains, "combine_issue_ms": round(work_ms, 3), "chain_latency_ms": round(lat_ms, 3),
+            "rank_ms": round(max(lat_ms, pass_ms + work_ms), 3)}
+
+
+def straus_report():
+    base = straus_row_model(1)["rank_ms"]
+    return [dict(straus_row_model(g), saving=round(1 - straus_row_model(g)["rank_ms"] / base, 3)) for g in (1, 2, 4, 5)]
+
+
 def interleave_report():
     rows = []
     for name, products, cus in (("whole-GPU combine, c5 one rank of G = 8 (D = 121 x T = 20)", 2420, 256),
@@ -215,6 +246,10 @@ if __name__ == "__main__":
     print("addition critical path (lane, row): %.0f, %.0f instructions" % p["add_chain_instr"])
     print("one G = 8 rank's combine (D = 120 x T = 20): per-lane model %.3f ms, row model %.3f ms: %.0f %% less"
           % (p["combine_ms_lane_model"], p["combine_ms_row_model"], 100 * p["saving"]))
+    print()
+    print("Straus in the row kernel, one G = 8 rank of c5 (D = 121, T = 20) beside its self-mask pass:")
+    for r in straus_report():
+        print("  ", r)
     print()
     print("two products interleaved per row (k = 2), cycles per formula step on one SIMD:")
     for name, r in interleave_report():
