@@ -48,10 +48,14 @@ def test_interleave_model_predicts_no_gain():
     assert R.interleave_model(2420, 256)["cycles_per_step_now"] > R.LONE_CPI      # D = 121 is issue-bound
 
 
-def test_straus_row_model_is_calibrated_and_clears_the_bar():
-    """Round 5: g terms of a pair per row chain.  g = 1 reproduces the measured one-rank-of-8
-    shares -> final (1.39-1.52 ms); g = 4 predicts >= 20 % less (built: ec_mul_row_straus_kernel)."""
+def test_straus_row_model_prediction_and_measurement():
+    """Round 5: g terms of a pair per row chain.  The model (g = 1 reproduces the measured one-rank-of-8
+    shares -> final, 1.39-1.52 ms) predicted >= 20 % less at g = 4, so it was built
+    (ec_mul_row_straus_kernel); measured, the chain ran 1.48x the latency the model assumed and the
+    rank gained 3 %: the default stays g = 1 (flm_set_tuning ec_row_terms)."""
     import ec_row_model as R
     rep = {r["g"]: r for r in R.straus_report()}
     assert R.RANK8_NOW_MS[0] - 0.05 <= rep[1]["rank_ms"] <= R.RANK8_NOW_MS[1]
     assert rep[4]["saving"] >= 0.2 and rep[2]["chain_latency_ms"] < rep[2]["rank_ms"]
+    assert 1 - R.MEASURED_RANK8_MS[4] / R.MEASURED_RANK8_MS[1] < 0.2             # measured: below the bar
+    assert R.MEASURED_COMBINE_MS[4] / rep[4]["chain_latency_ms"] > 1.4

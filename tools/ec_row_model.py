@@ -219,6 +219,14 @@ def straus_row_model(g, D=121, T=20, simds=SIMDS, pass_ms=PASS_MS_G8, adds_per_t
             "rank_ms": round(max(lat_ms, pass_ms + work_ms), 3)}
 
 
+# Measured after building it (profiles/r05_ec_row_straus_combine_alone.log, r05_rank8_row_straus.log):
+# the combine alone at D = 121 takes 0.825 / 0.994 / 1.405 ms at g = 1 / 2 / 4 -- the g = 4 chain runs
+# 1.48x the lone-wave latency the model assumed (0.95 ms: 4 LDS tables, 4 digit strings, up to 26
+# barriers per step against 8) -- and one rank's shares -> final 1.507 / 1.484 / 1.466 ms (-3 %).
+MEASURED_RANK8_MS = {1: 1.507, 2: 1.484, 4: 1.466}
+MEASURED_COMBINE_MS = {1: 0.825, 2: 0.994, 4: 1.405}
+
+
 def straus_report():
     base = straus_row_model(1)["rank_ms"]
     return [dict(straus_row_model(g), saving=round(1 - straus_row_model(g)["rank_ms"] / base, 3)) for g in (1, 2, 4, 5)]
