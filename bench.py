@@ -889,7 +889,8 @@ def measure_recovery(eng, torch, D, M, T, steps=10):
             "cpu_baseline": {"ms": best["ms"], "cores": best["cores"], "kind": "port",
                              "sample": f"the whole round, timed: Python big-int Lagrange of all {M} m_i, OpenSSL "
                                        f"EC_POINT_mul of all {D * T} lambda_j * share products (the reference's "
-                                       f"parallel_mult; pool = its multiprocessing.Pool over the {T} terms, "
+                                       f"parallel_mult; pool = its multiprocessing.Pool over the {T} terms "
+                                       f"(threads: ctypes releases the GIL in OpenSSL), "
                                        f"SA_ServiceAgent.py:552-572), EC_POINT_add sums, c1 - sum, SHA-256; its "
                                        f"seeds equal the GPU's",
                              "variants": base}}
@@ -940,29 +941,40 @@ def measure_h2c(eng, torch, reps=5, cpu_sample=4096):
     return res
 
 
+_TLS = None
+
+
 def _cpu_mul_column(args):
-    """One decryptor's column lambda_j * share_{j,i} (parallel_mult, SA_ServiceAgent.py:27-34), OpenSSL."""
+    """One decryptor's column lambda_j * share_{j,i} (parallel_mult, SA_ServiceAgent.py:27-34), OpenSSL,
+    on this thread's own curve context (flamingo_amd.crypto's module curve is not thread-safe)."""
+    import threading
+    global _TLS
     col, lam = args
     from flamingo_amd import crypto as C
+    if _TLS is None:
+        _TLS = threading.local()
+    cv = getattr(_TLS, "curve", None)
+    if cv is None:
+        cv = _TLS.curve = C._Curve()
     pts = C.points_from_wire(np.frombuffer(col, np.uint8).reshape(-1, 64))
-    return [C.mul(lam, p) for p in pts]
+    return [cv.mul(lam, p) for p in pts]
 
 
 def cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=1):
     """The reference's reconstruction seed recovery on the host, the whole round (not a sample):
     m_i = sum_j lambda_j y_{j,i} mod n (:518-526); for every dropout pair the T products
-    lambda_j share_{j,i} (:552-567; procs > 1: a process pool over the T terms, as the reference's
-    multiprocessing.Pool, started before the clock), their sum, c1 - sum, SHA-256 (:572-585)."""
+    lambda_j share_{j,i} (:552-567; procs > 1: one task per term j on a pool of `procs` workers, as
+    the reference's multiprocessing.Pool -- threads here, because ctypes releases the GIL inside
+    OpenSSL and a thread opens no extra process on the GPU box), their sum, c1 - sum, SHA-256
+    (:572-585)."""
     import hashlib
-    import multiprocessing as mp
-    from concurrent.futures import ProcessPoolExecutor
+    from concurrent.futures import ThreadPoolExecutor
     from flamingo_amd import crypto as C
     cols = [(dec[j * D:(j + 1) * D].tobytes(), lam[j]) for j in range(T)]
-    pool = None
-    if procs > 1:
-        pool = ProcessPoolExecutor(procs, mp_context=mp.get_context("spawn"))
-        list(pool.map(_cpu_mul_column, [(dec[:64].tobytes(), 1)] * procs))        # workers up
+    pool = ThreadPoolExecutor(procs) if procs > 1 else None
     try:
+        if pool:
+            list(pool.map(_cpu_mul_column, [(dec[:64].tobytes(), 1)] * procs))        # workers up
         t0 = time.perf_counter()
         seeds = [(sum(l * y[i] for l, y in zip(lam, ys)) % C.N).to_bytes(32, "big") for i in range(M)]
         t1 = time.perf_counter()

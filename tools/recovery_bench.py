@@ -11,10 +11,11 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from flamingo_amd import MaskEngine  # noqa: E402
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--D", type=int, default=962)
-ap.add_argument("--M", type=int, default=4055)
-ap.add_argument("--T", type=int, default=20)
-a = ap.parse_args()
-eng = MaskEngine(0)
-print(json.dumps(bench.measure_recovery(eng, torch, D=a.D, M=a.M, T=a.T)))
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--D", type=int, default=962)
+    ap.add_argument("--M", type=int, default=4055)
+    ap.add_argument("--T", type=int, default=20)
+    a = ap.parse_args()
+    eng = MaskEngine(0)
+    print(json.dumps(bench.measure_recovery(eng, torch, D=a.D, M=a.M, T=a.T)))
