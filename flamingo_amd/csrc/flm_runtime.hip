@@ -885,7 +885,7 @@ int flm_device_count(void) {
     return n;
 }
 
-const char *flm_version(void) { return "flamingo_hip 0.2 gfx950 items_kernel<S={1,4,16}>"; }
+const char *flm_version(void) { return "flamingo_hip 0.3 gfx950 items_kernel<S={1,4,16}>"; }
 
 int flm_init(flm_ctx **out, int device) {
     if (!out) return fail(nullptr, FLM_EINVAL, "flm_init: out is NULL");
