@@ -1998,19 +1998,24 @@ __device__ void h2c_map(const Fe &u_plain, Fe &x, Fe &y, bool &bad) {
 // msgs: n x kH2cMaxMsg bytes (message i in its first lens[i] bytes), or NULL for the decimal
 // strings of v0 + i (str(h_ijt), SA_ClientAgent.py:280).  out: n x 64 wire bytes (infinity: zeros,
 // flags bit 2); flags bit 3: no square root (not expected).
+// Two adjacent lanes per message: both expand it (9 SHA-256 compressions, cheap next to the field
+// work), lane 2m maps u_0 and lane 2m+1 maps u_1 -- the two map_to_curve calls are independent, so
+// the chain a lane runs is one inversion + two square roots instead of two of each -- then the odd
+// lane hands its point to the even one (a lane swap, no LDS), which adds, inverts and stores.
 __global__ __launch_bounds__(kEcThreads) void hash_to_curve_kernel(const uint8_t *__restrict__ msgs,
                                                                    const uint32_t *__restrict__ lens, uint32_t v0,
                                                                    int n, uint8_t *__restrict__ out,
                                                                    uint32_t *__restrict__ flags) {
-    const int i = blockIdx.x * kEcThreads + threadIdx.x;
-    if (i >= n) return;
+    const int t = blockIdx.x * kEcThreads + threadIdx.x;
+    const int i = t >> 1, half = t & 1;
+    const bool valid = i < n;  // both lanes of a pair stay to the swap: no early return
     uint8_t msg[kH2cMaxMsg];
     int m = 0;
-    if (msgs) {
+    if (valid && msgs) {
         m = (int)lens[i];
 #pragma unroll 1
         for (int k = 0; k < m; ++k) msg[k] = msgs[(size_t)i * kH2cMaxMsg + k];
-    } else {
+    } else if (valid) {
         uint32_t v = v0 + (uint32_t)i;
         uint8_t dig[10];
         int nd = 0;
@@ -2050,30 +2055,37 @@ __global__ __launch_bounds__(kEcThreads) void hash_to_curve_kernel(const uint8_t
 #pragma unroll
         for (int k = 0; k < 8; ++k) uni[(blk - 1) * 8 + k] = bi[k];
     }
-    Fe x0, y0, x1, y1;
-    bool bad0, bad1;
-    h2c_map(mod_n_384(uni), x0, y0, bad0);
-    h2c_map(mod_n_384(uni + 12), x1, y1, bad1);
+    Fe x, y;
+    bool bad;
+    h2c_map(mod_n_384(half ? uni + 12 : uni), x, y, bad);   // Q_half = map_to_curve(u_half)
+    Fe x1, y1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x1.v[k] = (uint32_t)__shfl_xor((int)x.v[k], 1);
+        y1.v[k] = (uint32_t)__shfl_xor((int)y.v[k], 1);
+    }
+    const bool bad1 = __shfl_xor((int)bad, 1) != 0;
+    if (!valid || half) return;
     Jac Q0, Q1;
-    Q0.X = x0;
-    Q0.Y = y0;
+    Q0.X = x;
+    Q0.Y = y;
     Q0.Z = fe_const(kOne);
     Q1.X = x1;
     Q1.Y = y1;
     Q1.Z = fe_const(kOne);
     const Jac R = jac_add(Q0, Q1);                                 // Q0 + Q1 (:282), P == +-Q handled
-    uint32_t fl = (bad0 || bad1) ? 8u : 0u;
-    Fe x = {}, y = {};
+    uint32_t fl = (bad || bad1) ? 8u : 0u;
+    Fe ax = {}, ay = {};
     if (fe_is_zero(R.Z)) {
         fl |= 4u;
     } else {
         const Fe zi = fe_inv(R.Z);
         const Fe zi2 = fe_sqr(zi);
-        x = from_mont(fe_mul(R.X, zi2));
-        y = from_mont(fe_mul(R.Y, fe_mul(zi2, zi)));
+        ax = from_mont(fe_mul(R.X, zi2));
+        ay = from_mont(fe_mul(R.Y, fe_mul(zi2, zi)));
     }
-    store_be(out + (size_t)i * 64, x);
-    store_be(out + (size_t)i * 64 + 32, y);
+    store_be(out + (size_t)i * 64, ax);
+    store_be(out + (size_t)i * 64 + 32, ay);
     flags[i] = fl;
 }
 
@@ -2173,8 +2185,9 @@ hipError_t launch_ec_finish(const uint8_t *d_base, const uint32_t *d_jac, int T,
 hipError_t launch_hash_to_curve(const uint8_t *d_msgs, const uint32_t *d_lens, uint32_t v0, int n, uint8_t *d_out,
                                 uint32_t *d_flags, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hash_to_curve_kernel, dim3((unsigned)((n + kEcThreads - 1) / kEcThreads)), dim3(kEcThreads), 0,
-                       stream, d_msgs, d_lens, v0, n, d_out, d_flags);
+    const size_t lanes = 2 * (size_t)n;  // two lanes per message
+    hipLaunchKernelGGL(hash_to_curve_kernel, dim3((unsigned)((lanes + kEcThreads - 1) / kEcThreads)), dim3(kEcThreads),
+                       0, stream, d_msgs, d_lens, v0, n, d_out, d_flags);
     return hipGetLastError();
 }
 
