@@ -299,8 +299,8 @@ __device__ __forceinline__ Fe from_mont(const Fe &a) {
 #ifndef FLM_INV_BINGCD
 #define FLM_INV_BINGCD 1
 #endif
+#if !FLM_INV_BINGCD
 // a^(p-2): p-2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
-// (0 -> 0, which hash-to-curve's map relies on; ec_finish uses it only with FLM_INV_BINGCD=0)
 __device__ Fe fe_inv(const Fe &a) {
     // x_k = a^(2^k - 1)
     Fe x2 = fe_mul(fe_sqr(a), a);
@@ -339,6 +339,7 @@ __device__ Fe fe_inv(const Fe &a) {
     r = fe_mul(r, a);                       // 1
     return r;
 }
+#endif  // !FLM_INV_BINGCD
 
 // ---- inversion by binary GCD (ec_finish_kernel's one-lane chain)
 // Pornin, "Optimized Binary GCD for Modular Inversion" (eprint 2020/972), Algorithm 2, with
@@ -1955,6 +1956,13 @@ __device__ Fe mod_n_384(const uint32_t *u) {
     return r;
 }
 
+// Montgomery-form inverse by binary GCD (ec_finish_kernel's: ~25k VALU instructions against Fermat's
+// ~73k): (a R)^-1 R^3 R^-1 = a^-1 R; 0 -> 0, as the reference's tv1 branch needs
+__device__ __forceinline__ Fe fe_inv_mont(const Fe &a) {
+    if (fe_is_zero(a)) return a;
+    return fe_mul(fe_inv_bingcd(a), fe_const(kR3));
+}
+
 __device__ __forceinline__ Fe fe_sqr_n(Fe a, int n) {
 #pragma unroll 1
     for (int i = 0; i < n; ++i) a = fe_sqr(a);
@@ -1980,7 +1988,7 @@ __device__ void h2c_map(const Fe &u_plain, Fe &x, Fe &y, bool &bad) {
     const Fe u2 = fe_sqr(u);
     const Fe u4 = fe_sqr(u2);
     const Fe den = fe_sub(fe_mul(fe_const(k100m), u4), fe_mul(fe_const(k10m), u2));
-    const Fe tv1 = fe_inv(den);                                   // 0 -> 0 (the :247-248 branch)
+    const Fe tv1 = fe_inv_mont(den);                              // 0 -> 0 (the :247-248 branch)
     Fe x1 = fe_mul(fe_const(kC1m), fe_add(fe_const(kOne), tv1));
     if (fe_is_zero(tv1)) x1 = fe_const(kC2m);
     const Fe gx1 = fe_add(fe_mul(x1, fe_add(fe_sqr(x1), fe_const(kAm))), fe_const(kBm));
@@ -2079,7 +2087,7 @@ __global__ __launch_bounds__(kEcThreads) void hash_to_curve_kernel(const uint8_t
     if (fe_is_zero(R.Z)) {
         fl |= 4u;
     } else {
-        const Fe zi = fe_inv(R.Z);
+        const Fe zi = fe_inv_mont(R.Z);
         const Fe zi2 = fe_sqr(zi);
         ax = from_mont(fe_mul(R.X, zi2));
         ay = from_mont(fe_mul(R.Y, fe_mul(zi2, zi)));
