@@ -106,3 +106,46 @@ def test_shard_bounds_properties():
                 assert hi == lo2 and (lo % 16 == 0 or lo == hi)
             assert padded_length(L, G) % (1024 * G) == 0
             assert sum(client_bounds(1000, G, r)[1] - client_bounds(1000, G, r)[0] for r in range(G)) == 1000
+
+
+class _LoggingEngine:
+    """Stands in for a MaskEngine in distributed.shutdown (isinstance is patched to accept it)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def comm_destroy(self):
+        self.calls.append("comm_destroy")
+
+    def close(self):
+        self.calls.append("close")
+
+
+def shutdown_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flamingo_amd import distributed as D
+    from flamingo_amd import engine as E
+    E.MaskEngine = _LoggingEngine                       # shutdown's isinstance check sees the stand-in
+    eng = _LoggingEngine()
+    D.shutdown(eng)
+    q.put((rank, eng.calls, dist.is_initialized()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shutdown_tears_down_a_real_process_group(world):
+    """distributed.shutdown on every rank of a real (gloo) world: library communicator first, the
+    barrier, destroy_process_group, then the contexts -- no rank hangs, every rank ends uninitialised."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=shutdown_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [g[0] for g in got] == list(range(world))
+    for _, calls, still_init in got:
+        assert calls == ["comm_destroy", "close"] and not still_init
