@@ -19,7 +19,6 @@ sk_j * c0 for each dropout ciphertext plus their decrypted m_i shares
 """
 from __future__ import annotations
 
-import hashlib
 import logging
 
 import numpy as np
@@ -46,12 +45,11 @@ def pair_prf(engine, keys, iteration: int) -> list:
     if not keys:
         return []
     rnd = int(iteration).to_bytes(16, "big")[:4]
-    ks0 = engine.prg_expand(list(keys), 1)[:, 0] ^ np.uint32(0x64636261)
-    out = []
-    for w in ks0:
-        h = bytes(a ^ b for a, b in zip(int(w).to_bytes(4, "little"), rnd))
-        out.append(str(int.from_bytes(h, "big") & 0xFFFF))
-    return out
+    w = np.asarray(engine.prg_expand(list(keys), 1))[:, 0].astype(np.uint32) ^ np.uint32(0x64636261)
+    # ciphertext byte k = keystream byte k (LE byte k of word 0) ^ rnd[k]; h = bytes 2..3, big endian
+    b2 = ((w >> np.uint32(16)) & np.uint32(0xFF)) ^ np.uint32(rnd[2])
+    b3 = ((w >> np.uint32(24)) & np.uint32(0xFF)) ^ np.uint32(rnd[3])
+    return [str(v) for v in ((b2 << np.uint32(8)) | b3).tolist()]
 
 class SA_ClientAgent(Agent):
     def __str__(self):
@@ -89,7 +87,6 @@ class SA_ClientAgent(Agent):
         self.secret_key = pki.client_sk[id]
         self.public_key = pki.client_pk[id]
         self.system_pk = pki.system_pk
-        self.pair_keys = {}          # neighbour -> SHA-256(a_i A_j)[:32]   (:256-263), cached across iterations
         self.committee_keys = {}     # member -> AES key (a_i A_c).x mod 2^128 (:234-236)
         self.symmetric_keys = {}     # (committee members) client -> AES key (:86-91)
         param.register_client(self)
@@ -165,14 +162,8 @@ class SA_ClientAgent(Agent):
         if self.id in self.neighbors_list:
             raise RuntimeError("id itself appears in its neighbor list")
         committee = sorted(self.user_committee)
-        # ECDH keys (cached: keys do not change between iterations); the whole iteration's graph
-        # is one GPU batch (protocol.prefetch_graph_ecdh)
-        missing = [j for j in nb if j not in self.pair_keys]
-        if missing:
-            param.prefetch_graph_ecdh(self.current_iteration, self.num_clients, self.neighborhood_size)
-            for j in missing:
-                w = param.ecdh_wire(self.num_clients, self.id, j)
-                self.pair_keys[j] = hashlib.sha256(w).digest()[: self.key_length]
+        # the ECDH keys r_ij = SHA-256(a_i A_j) of the whole iteration's graph: one GPU batch, cached in
+        # the protocol (pair_material below)
         if not self.committee_keys:
             self.committee_keys = self._aes_keys(committee)
 
@@ -188,19 +179,21 @@ class SA_ClientAgent(Agent):
             ct, _ = C.aes_gcm_encrypt(self.committee_keys[cid], y.to_bytes(self.key_length, "big"), nonce)
             enc_mi_shares.append((ct, nonce))
 
-        # pairwise seeds: h_ijt -> H (group element) -> s_ij (:266-292)
-        H, seeds, signs = {}, [mi_bytes], [1]
-        for j, h in zip(nb, pair_prf(param.engine(), [self.pair_keys[j] for j in nb], self.current_iteration)):
-            H[j] = param.hash_to_curve(h)
-            seeds.append(hashlib.sha256(C.point_bytes(H[j])).digest()[: self.key_length])
-            signs.append(1 if self.id < j else -1)
+        # pairwise seeds: h_ijt -> H (group element) -> s_ij (:266-292), every client's in a few
+        # batched launches (protocol.pair_material: one PRG launch for all h_ijt, the hash-to-curve table)
+        pnb, _, _, s_ij = param.pair_material(self.current_iteration, self.num_clients,
+                                              self.neighborhood_size)[self.id]
+        if pnb != nb:
+            raise RuntimeError("pair material built for another neighbour order")
+        seeds = [mi_bytes] + [s[: self.key_length] for s in s_ij]
+        signs = [1] + [1 if self.id < j else -1 for j in nb]
 
-        # ElGamal under the system key: c0 = rG, c1 = H + r pk (:434-447); the r G, r pk of every
-        # client of the iteration come from one GPU batch (protocol.elgamal_masks)
-        _, rg, rpk = param.elgamal_masks(self, self.current_iteration, nb)
+        # ElGamal under the system key: c0 = rG, c1 = H + r pk (:326-332, :434-447); every client's
+        # r G and H + r pk of the iteration come from two GPU launches (protocol.elgamal_masks)
+        _, rg, c1w = param.elgamal_masks(self, self.current_iteration, nb)
         c0 = C.points_from_wire(rg) if nb else []
-        rp = C.points_from_wire(rpk) if nb else []
-        cipher = {(self.id, j): (c0[k], C.add(H[j], rp[k])) for k, j in enumerate(nb)}
+        c1 = C.points_from_wire(c1w) if nb else []
+        cipher = {(self.id, j): (c0[k], c1[k]) for k, j in enumerate(nb)}
 
         x = None if self.input_vector is None else np.asarray(self.input_vector, np.uint32)[None, :]
         vec = param.engine().client_mask(np.array([0, len(seeds)], np.int64), seeds, signs, self.vector_len, x=x)[0]

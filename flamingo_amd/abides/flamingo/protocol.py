@@ -37,7 +37,9 @@ _h2c_table = None         # (out (65536, 64), flags): hash_str_to_curve(str(v)) 
 _ecdh: dict = {}          # (root, N, min(i,j), max(i,j)) -> 64-byte wire of a_i A_j
 _ecdh_done: set = set()   # batches already computed (graph iterations, committee)
 _clients: dict = {}       # id -> client agent (for the batched ElGamal draws)
-_elgamal: dict = {}       # (root, iteration, id) -> (r list, (deg, 64) rG wire, (deg, 64) r pk wire)
+_elgamal: dict = {}       # (root, iteration, id) -> (r list, (deg, 64) rG wire, (deg, 64) c1 = H + r pk wire)
+_pair_keys: dict = {}     # (root, N, min(i,j), max(i,j)) -> r_ij = SHA-256(a_i A_j)[:32] (symmetric)
+_pair_mat: dict = {}      # (root, iteration, N, nsize) -> {id: PairMaterial}
 
 
 def configure(root: bytes | None = None, L: int | None = None, committee: int | None = None):
@@ -58,6 +60,8 @@ def configure(root: bytes | None = None, L: int | None = None, committee: int | 
     _ecdh_done.clear()
     _clients.clear()
     _elgamal.clear()
+    _pair_keys.clear()
+    _pair_mat.clear()
     _h2c.clear()                 # the table is the engine's: recomputed with whatever engine is current
     _h2c_table = None
 
@@ -238,14 +242,65 @@ def ecdh_wire(num_clients: int, i: int, j: int) -> bytes:
     return _ecdh[k]
 
 
+def h2c_table():
+    """(out (65536, 64), flags) of hash_str_to_curve(str(v)) for every v < 2^16, one GPU launch
+    (computed on first use, kept for the simulation)."""
+    global _h2c_table
+    if _h2c_table is None:
+        _h2c_table = engine().hash_to_curve_decimal(0, 1 << 16)
+    return _h2c_table
+
+
+def pair_material(iteration: int, num_clients: int, neighborhood_size: int) -> dict:
+    """Every client's pairwise seeds of `iteration` in a few batched launches
+    (SA_ClientAgent.py:253-292): id -> (nb, h, H, s) with nb the neighbour list in the reference's
+    set order, h the h_ijt strings, H the (deg, 64) wire rows of hash_str_to_curve(h_ijt) and s the
+    32-byte seeds SHA-256(H).  r_ij = SHA-256(a_i A_j) comes from the graph's ECDH batch; every h_ijt
+    of the iteration from ONE PRG launch (client_agent.pair_prf); H from the hash-to-curve table."""
+    import hashlib
+    import numpy as np
+    key = (root_seed, iteration, num_clients, neighborhood_size)
+    if key in _pair_mat:
+        return _pair_mat[key]
+    from .client_agent import pair_prf
+    nbrs = neighbors(iteration, num_clients, neighborhood_size)
+    prefetch_graph_ecdh(iteration, num_clients, neighborhood_size)
+    lists = [list(nbrs[i]) for i in range(num_clients)]
+    keys = []
+    for i, nb in enumerate(lists):
+        for j in nb:
+            k = (root_seed, num_clients, min(i, j), max(i, j))
+            r = _pair_keys.get(k)
+            if r is None:
+                r = _pair_keys[k] = hashlib.sha256(ecdh_wire(num_clients, i, j)).digest()[:32]
+            keys.append(r)
+    hs = pair_prf(engine(), keys, iteration)
+    out, fl = h2c_table()
+    rows = [np.asarray(out[int(h)], np.uint8) for h in hs]
+    mat, o = {}, 0
+    for i, nb in enumerate(lists):
+        n = len(nb)
+        H = np.stack(rows[o:o + n]) if n else np.zeros((0, 64), np.uint8)
+        if n and any(int(fl[int(h)]) & 4 for h in hs[o:o + n]):
+            raise RuntimeError("hash_to_curve gave the point at infinity")      # not in the 2^16 table
+        mat[i] = (nb, hs[o:o + n], H, [hashlib.sha256(r.tobytes()).digest() for r in H])
+        o += n
+    for k in [k for k in _pair_mat if k[1] < iteration - 1]:
+        del _pair_mat[k]
+    _pair_mat[key] = mat
+    return mat
+
+
 def register_client(agent) -> None:
     _clients[agent.id] = agent
 
 
 def elgamal_masks(agent, iteration: int, nb: list):
-    """(r list, r G wire rows, r pk_system wire rows) for this client's neighbours in `iteration`
-    (SA_ClientAgent.py:434-447).  The first client to ask in an iteration draws every registered,
-    online client's r's from that client's own random state and computes all of them in one launch."""
+    """(r list, c0 = r G wire rows, c1 = H + r pk_system wire rows) for this client's neighbours in
+    `iteration` (SA_ClientAgent.py:326-332, 434-447), H the pair's hash-to-curve point
+    (pair_material).  The first client to ask in an iteration draws every registered, online
+    client's r's from that client's own random state and computes all of them in two launches:
+    r G and r pk (flm_ec_mul), then H + r pk (flm_ec_combine with one term of coefficient 1)."""
     from ... import crypto as C
     import numpy as np
     key = (root_seed, iteration, agent.id)
@@ -266,11 +321,16 @@ def elgamal_masks(agent, iteration: int, nb: list):
                                    np.tile(np.frombuffer(C.point_bytes(sys_pk), np.uint8), (len(rs), 1))])
             out, _ = engine().ec_mul_wire(base, C.scalars_to_wire(rs + rs))
             out = np.asarray(out)
+            pm = pair_material(iteration, agent.num_clients, agent.neighborhood_size)
+            H = np.concatenate([pm[cid][2] for cid, r_list in batch if r_list])
+            c1, _, fl = engine().ec_combine_wire(H, out[len(rs):][None], C.scalars_to_wire([1]), negate=False)
+            c1 = np.asarray(c1)
+            if (np.asarray(fl) & 4).any():
+                raise RuntimeError("ElGamal c1 = H + r pk at infinity")
         o = 0
         for cid, r_list in batch:
             n = len(r_list)
-            _elgamal[(root_seed, iteration, cid)] = (r_list, out[o:o + n] if n else None,
-                                                     out[len(rs) + o:len(rs) + o + n] if n else None)
+            _elgamal[(root_seed, iteration, cid)] = (r_list, out[o:o + n] if n else None, c1[o:o + n] if n else None)
             o += n
         for k in [k for k in _elgamal if k[1] < iteration - 1]:
             del _elgamal[k]
