@@ -89,6 +89,7 @@ SIGNATURES = {
     "flm_store_partial_wait": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "flm_store_partial_host": (_int, [_vp, _u32p]),
     "flm_store_unmask": (_int, [_vp, _u8p, _i8p, _int, _u32p]),
+    "flm_store_unmask_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "flm_store_reset": (_int, [_vp]),
     "flm_host_alloc": (_vp, [_sz]),
     "flm_host_free": (None, [_vp]),

@@ -140,7 +140,8 @@ def run(argv=None):
         gpu = server.gpu_ms.get(it, {})
         print(f"    iteration {it}: |U| = {u}, dropout pairs = {server.pairs_per_iteration.get(it, 0)}, "
               f"final_sum == |U| in every slot: {bool(np.all(out == u))}; report GPU {gpu.get('report', 0):.3f} ms, "
-              f"unmask + D2H {gpu.get('reconstruction_unmask_wall', 0):.3f} ms")
+              f"unmask + D2H {gpu.get('reconstruction_unmask_gpu', 0):.3f} ms GPU "
+              f"({gpu.get('reconstruction_unmask_wall', 0):.3f} ms wall)")
     print()
     results["server"] = server
     return results

@@ -325,8 +325,13 @@ class SA_ServiceAgent(Agent):
             # setter, :540/:605) is the S the masks are added to, on the GPU
             self.final_sum = param.engine().mask_accumulate(seeds, signs, self._host_partial.copy())
         ms = (pd.Timestamp("now") - t0).total_seconds() * 1e3
-        self.gpu_ms.setdefault(self.current_iteration, {})["reconstruction_unmask_wall"] = ms
-        self.agent_print(f"reconstruction unmask: {len(seeds)} masks over S on the GPU(s) + D2H, {ms:.3f} ms")
+        rec = self.gpu_ms.setdefault(self.current_iteration, {})
+        rec["reconstruction_unmask_wall"] = ms
+        gpu = st.unmask_ms() if hasattr(st, "unmask_ms") and getattr(st, "has_partial", False) else None
+        if gpu is not None:
+            rec["reconstruction_unmask_gpu"] = gpu
+        self.agent_print(f"reconstruction unmask: {len(seeds)} masks over S on the GPU(s) + D2H, {ms:.3f} ms wall"
+                         + (f", {gpu:.3f} ms GPU" if gpu is not None else ""))
         self.results[self.current_iteration] = self.final_sum
         self.online_counts[self.current_iteration] = len(self.user_vectors)
         self.pairs_per_iteration[self.current_iteration] = len(self.recon_symbol)

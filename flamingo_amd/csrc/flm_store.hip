@@ -60,6 +60,8 @@ struct flm_store {
     int bad = 0;                 // bodies of the wrong length since the last reset
     bool have_partial = false;
     hipEvent_t t0 = nullptr, t1 = nullptr;  // device time of the last partial sum (rank 0)
+    hipEvent_t u0 = nullptr, u1 = nullptr;  // device time of the last unmask, uploads to D2H (rank 0)
+    float unmask_ms = -1.0f;
     std::string err;
 };
 
@@ -125,6 +127,8 @@ void release(flm_store *st) {
     }
     if (st->t0) (void)hipEventDestroy(st->t0);
     if (st->t1) (void)hipEventDestroy(st->t1);
+    if (st->u0) (void)hipEventDestroy(st->u0);
+    if (st->u1) (void)hipEventDestroy(st->u1);
 }
 
 }  // namespace
@@ -174,7 +178,8 @@ int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int 
     }
     if (!rc) {
         (void)hipSetDevice(st->rk[0].device);
-        if (hipEventCreate(&st->t0) != hipSuccess || hipEventCreate(&st->t1) != hipSuccess)
+        if (hipEventCreate(&st->t0) != hipSuccess || hipEventCreate(&st->t1) != hipSuccess ||
+            hipEventCreate(&st->u0) != hipSuccess || hipEventCreate(&st->u1) != hipSuccess)
             rc = sfail(st, FLM_EHIP, "flm_store_create: hipEventCreate");
     }
     if (rc) {
@@ -319,6 +324,9 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
     for (int k = 0; k < K; ++k)
         if (signs[k] != 1 && signs[k] != -1) return sfail(st, FLM_EINVAL, "signs must be +1 or -1");
     const size_t sb = (size_t)K * 33;
+    st->unmask_ms = -1.0f;
+    FLM_SHIP(st, hipSetDevice(st->rk[0].device));
+    FLM_SHIP(st, hipEventRecord(st->u0, flm::rt::stream_of(st->rk[0].ctx)));
     for (StoreRank &k : st->rk) {
         const size_t n = k.hi - k.lo;
         if (n == 0) continue;
@@ -343,10 +351,21 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
             return sfail(st, rc, std::string("store unmask: ") + flm_last_error(k.ctx));
         FLM_SHIP(st, hipMemcpyAsync(out + k.lo, k.out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
+    FLM_SHIP(st, hipSetDevice(st->rk[0].device));
+    FLM_SHIP(st, hipEventRecord(st->u1, flm::rt::stream_of(st->rk[0].ctx)));
     for (StoreRank &k : st->rk) {
         FLM_SHIP(st, hipSetDevice(k.device));
         FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
     }
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, st->u0, st->u1) == hipSuccess) st->unmask_ms = ms;
+    return 0;
+}
+
+int flm_store_unmask_ms(const flm_store *st, float *gpu_ms) {
+    if (!st || !gpu_ms) return FLM_EINVAL;
+    if (st->unmask_ms < 0.0f) return sfail(const_cast<flm_store *>(st), FLM_EINVAL, "no unmask has completed");
+    *gpu_ms = st->unmask_ms;
     return 0;
 }
 

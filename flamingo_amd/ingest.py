@@ -122,3 +122,9 @@ class VectorStore:
         self._check(self.lib.flm_store_unmask(self.h, p_u8(seeds), p_i8(signs), seeds.shape[0], p_u32(out)),
                     "flm_store_unmask")
         return out
+
+    def unmask_ms(self) -> float:
+        """Device time (ms) of the last unmask, seed upload to the end of the D2H (flm_store_unmask_ms)."""
+        ms = ctypes.c_float()
+        self._check(self.lib.flm_store_unmask_ms(self.h, ctypes.byref(ms)), "flm_store_unmask_ms")
+        return float(ms.value)

@@ -387,6 +387,9 @@ int flm_store_partial(flm_store *st);
 int flm_store_partial_wait(flm_store *st, float *gpu_ms);
 int flm_store_partial_host(flm_store *st, uint32_t *out);
 int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *out);
+/* Device time (ms, rank 0's stream) of the last flm_store_unmask, from its seed upload to the end of
+ * its copy of final_sum to the host: the part of the call's wall time the GPU accounts for. */
+int flm_store_unmask_ms(const flm_store *st, float *gpu_ms);
 int flm_store_reset(flm_store *st);
 
 /* Allocate / free page-locked host memory through HIP (for a pinned arena

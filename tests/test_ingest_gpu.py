@@ -52,6 +52,7 @@ def test_store_round_vs_oracle(G, N, K, L):
             got = st.unmask(seeds, signs)
             want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
             assert np.array_equal(got, want), (G, N, K, L, it)
+            assert st.unmask_ms() > 0.0                          # the call's device time (flm_store_unmask_ms)
             st.reset()
         st.close()
     finally:
