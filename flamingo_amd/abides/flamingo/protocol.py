@@ -182,14 +182,11 @@ def hash_to_curve(h_ijt: str):
     computes the whole table of the 2^16 possible points in one launch
     (MaskEngine.hash_to_curve_decimal) and every later call is a lookup; any other message is
     hashed by its own launch.  Returns the affine point (x, y), or None for infinity."""
-    global _h2c_table
     pt = _h2c.get(h_ijt)
     if pt is not None:
         return pt
     if h_ijt.isdigit() and str(int(h_ijt)) == h_ijt and int(h_ijt) < (1 << 16):
-        if _h2c_table is None:
-            _h2c_table = engine().hash_to_curve_decimal(0, 1 << 16)
-        out, fl = _h2c_table
+        out, fl = h2c_table()
         row, f = out[int(h_ijt)], int(fl[int(h_ijt)])
     else:
         out, fl = engine().hash_to_curve_wire([h_ijt])
