@@ -19,7 +19,15 @@ def main(argv=None):
     if args.config != "flamingo":
         raise SystemExit(f"config {args.config!r} is not part of this repository (only 'flamingo')")
     from .config_flamingo import run
-    run(argv)
+    from .flamingo import protocol
+    res = run(argv)
+    # explicit teardown (the server's store, its device group and RCCL clique, the engine) instead of
+    # leaving them to finalizers at interpreter exit
+    if res is not None:
+        srv = res.get("server")
+        if srv is not None and srv._store is not None:
+            srv._store.close()
+    protocol.shutdown()
 
 
 if __name__ == "__main__":

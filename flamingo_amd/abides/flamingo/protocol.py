@@ -66,6 +66,19 @@ def configure(root: bytes | None = None, L: int | None = None, committee: int | 
     _h2c_table = None
 
 
+def shutdown():
+    """Close the server's device group (its RCCL clique included) and the process engine, after the
+    stores on them are closed; the next engine()/server_engine() call starts afresh."""
+    global _engine, _group
+    configure()
+    if _group is not None:
+        _group.close()
+        _group = None
+    if _engine is not None:
+        _engine.close()
+        _engine = None
+
+
 def engine():
     """The process's MaskEngine (created lazily: after any fork, before first use)."""
     global _engine

@@ -169,3 +169,19 @@ def test_ec_combine_restores_the_callers_ec_coop():
     rec._ec_combine(None, None, None, None, None)
     assert eng.seen == 1 and eng.t["ec_coop"] == 2
     assert torch.device("cpu") == rec.device
+
+
+def test_protocol_shutdown_closes_group_and_engine(fake_groups):
+    """The simulation's explicit teardown (python -m flamingo_amd.abides ends with it): the group, then
+    the engine; nothing left to an exit-time finalizer."""
+    fake_groups.setenv("FLM_GROUP_DEVICES", "0,1")
+    g = protocol.server_engine()
+    closed = []
+
+    class Eng:
+        def close(self):
+            closed.append("engine")
+
+    fake_groups.setattr(protocol, "_engine", Eng())
+    protocol.shutdown()
+    assert g.closed and closed == ["engine"] and protocol._group is None and protocol._engine is None
