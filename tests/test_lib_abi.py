@@ -55,3 +55,18 @@ def test_gfx950_code_object(lib):
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
     assert b"items_kernel" in data
+
+
+def test_round5_entry_points_reject_null_handles(lib):
+    """flm_comm_destroy, flm_hash_to_curve*, flm_store_unmask_ms: a NULL context / store is an
+    FLM_EINVAL with a message, before any device call (no GPU needed)."""
+    buf = (ctypes.c_uint8 * 64)()
+    fl = (ctypes.c_uint32 * 1)()
+    ln = (ctypes.c_uint32 * 1)(3)
+    assert lib.flm_comm_destroy(None) == -1 and b"NULL" in lib.flm_last_error(None)
+    assert lib.flm_hash_to_curve(None, buf, ln, 1, buf, fl) == -1
+    assert lib.flm_hash_to_curve_decimal(None, 0, 1, buf, fl) == -1
+    assert lib.flm_hash_to_curve_decimal_dev(None, 0, 1, None, None, None) == -1
+    ms = ctypes.c_float()
+    assert lib.flm_store_unmask_ms(None, ctypes.byref(ms)) == -1
+    assert b"0.3" in lib.flm_version()
