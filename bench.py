@@ -878,7 +878,7 @@ def measure_recovery(eng, torch, D, M, T, steps=10):
     want_m = [(sum(l * y[i] for l, y in zip(lam, ys)) % C.N).to_bytes(32, "big") for i in range(M)]
     ok &= all(bytes(got_seeds[i]) == want_m[i] for i in range(M))
     base = {"1_core": cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=1)}
-    procs = min(host_threads()[0], T)
+    procs = min(host_threads()[0], T, CPU_POOL_MAX)
     if procs > 1:
         base["pool"] = cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=procs)
     for b in base.values():
@@ -889,8 +889,8 @@ def measure_recovery(eng, torch, D, M, T, steps=10):
             "cpu_baseline": {"ms": best["ms"], "cores": best["cores"], "kind": "port",
                              "sample": f"the whole round, timed: Python big-int Lagrange of all {M} m_i, OpenSSL "
                                        f"EC_POINT_mul of all {D * T} lambda_j * share products (the reference's "
-                                       f"parallel_mult; pool = its multiprocessing.Pool over the {T} terms "
-                                       f"(threads: ctypes releases the GIL in OpenSSL), "
+                                       f"parallel_mult; pool = its multiprocessing.Pool over the {T} terms, "
+                                       f"{procs} spawned workers), "
                                        f"SA_ServiceAgent.py:552-572), EC_POINT_add sums, c1 - sum, SHA-256; its "
                                        f"seeds equal the GPU's",
                              "variants": base}}
@@ -944,9 +944,12 @@ def measure_h2c(eng, torch, reps=5, cpu_sample=4096):
 _TLS = None
 
 
+CPU_POOL_MAX = 8   # spawned CPU-baseline workers (each may open the GPU under rocprofv3; the box allows 16)
+
+
 def _cpu_mul_column(args):
     """One decryptor's column lambda_j * share_{j,i} (parallel_mult, SA_ServiceAgent.py:27-34), OpenSSL,
-    on this thread's own curve context (flamingo_amd.crypto's module curve is not thread-safe)."""
+    on a curve context of this worker's own."""
     import threading
     global _TLS
     col, lam = args
@@ -963,15 +966,18 @@ def _cpu_mul_column(args):
 def cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=1):
     """The reference's reconstruction seed recovery on the host, the whole round (not a sample):
     m_i = sum_j lambda_j y_{j,i} mod n (:518-526); for every dropout pair the T products
-    lambda_j share_{j,i} (:552-567; procs > 1: one task per term j on a pool of `procs` workers, as
-    the reference's multiprocessing.Pool -- threads here, because ctypes releases the GIL inside
-    OpenSSL and a thread opens no extra process on the GPU box), their sum, c1 - sum, SHA-256
-    (:572-585)."""
+    lambda_j share_{j,i} (:552-567; procs > 1: one task per term j on a pool of `procs` spawned
+    worker processes, as the reference's multiprocessing.Pool), their sum, c1 - sum, SHA-256
+    (:572-585).  At most CPU_POOL_MAX workers: under rocprofv3 every spawned worker inherits the
+    profiler's preload and opens the GPU, and the box allows 16 processes on it (16 workers + this
+    one tripped that guard once); threads were tried instead and lose to the GIL (1,061 ms on 16
+    against 777 on one core)."""
     import hashlib
-    from concurrent.futures import ThreadPoolExecutor
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
     from flamingo_amd import crypto as C
     cols = [(dec[j * D:(j + 1) * D].tobytes(), lam[j]) for j in range(T)]
-    pool = ThreadPoolExecutor(procs) if procs > 1 else None
+    pool = ProcessPoolExecutor(procs, mp_context=mp.get_context("spawn")) if procs > 1 else None
     try:
         if pool:
             list(pool.map(_cpu_mul_column, [(dec[:64].tobytes(), 1)] * procs))        # workers up
