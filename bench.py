@@ -497,7 +497,7 @@ def main():
             }
             c5 = res["other_configs"]["c5"]
             rec = measure_recovery(eng, torch, D=int(round(c5["dropout_pairs_D_mean"])),
-                                   M=int(round(c5["online_mean"])), T=20)
+                                   M=int(round(c5["online_mean"])), T=20, cpu_pool=True)
             rec["server_reconstruction_ms"] = round(rec["gpu_ms"] + c5["ms_per_round"], 4)
             c5["seed_recovery"] = rec
             # one rank's share on 8 GPUs (dist_recon: every rank recovers all m_i and ceil(D/8) pairs):
@@ -820,7 +820,7 @@ def time_exchange(torch, dist, rnd, stream, coll_dev, L, reps=10):
             "bus_GB_per_s": round(nbytes * (rnd.world - 1) / rnd.world / (ms * 1e-3) / 1e9, 1)}
 
 
-def measure_recovery(eng, torch, D, M, T, steps=10):
+def measure_recovery(eng, torch, D, M, T, steps=10, cpu_pool=False):
     """Seed recovery of one c5 round on the GPU (SA_ServiceAgent.py:506-526, 542-585):
     M self-mask seeds m_i = sum_j lambda_j y_{j,i} mod n and D dropout-pair seeds
     SHA-256(c1_i - sum_j lambda_j sk_j c0_i), T = 20 decryptors (committee 60, fraction 1/3).
@@ -879,7 +879,9 @@ def measure_recovery(eng, torch, D, M, T, steps=10):
     ok &= all(bytes(got_seeds[i]) == want_m[i] for i in range(M))
     base = {"1_core": cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=1)}
     procs = min(host_threads()[0], T, CPU_POOL_MAX)
-    if procs > 1:
+    # cpu_pool: only from a script whose top level is main-guarded (bench.py, tools/recovery_bench.py):
+    # spawned workers re-import the caller's main module
+    if cpu_pool and procs > 1:
         base["pool"] = cpu_seed_recovery(dec, c1, lam, ys, M, D, T, procs=procs)
     for b in base.values():
         ok &= b.pop("seeds") == [bytes(x) for x in got_seeds]

@@ -18,4 +18,4 @@ if __name__ == "__main__":
     ap.add_argument("--T", type=int, default=20)
     a = ap.parse_args()
     eng = MaskEngine(0)
-    print(json.dumps(bench.measure_recovery(eng, torch, D=a.D, M=a.M, T=a.T)))
+    print(json.dumps(bench.measure_recovery(eng, torch, D=a.D, M=a.M, T=a.T, cpu_pool=True)))
