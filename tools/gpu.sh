@@ -10,6 +10,9 @@
 #   benchG:N     bench.py --gpus N --dist-backend gloo --steps 3 (N self-launched ranks on the one GPU:
 #                the sharded c4 and c5 paths end to end, correctness only)
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
+#   simc3 / simc5 / simc5r   the agents at BASELINE c3, c5 (n=4096, L=2^20, 10 iterations, 1 % dropouts), reduced c5
+#   simprof      cProfile of the reduced c5 run;  simtrace  rocprofv3 kernel trace of a 4-iteration c5 run
+#   h2c          the hash-to-curve table launch under a kernel trace;  ecstraus  Straus-in-row EC measurements
 #   rccl         tools/rccl_clique_smoke.py (forced one-device RCCL clique + world-1 forced collectives),
 #                then the same with AMD_LOG_LEVEL=4: the kernels it dispatched (RCCL's included)
 #   rccltrace    the same script under rocprofv3 --kernel-trace --stats (put it last in a call)
@@ -67,6 +70,23 @@ for step in "$@"; do
       python -c "import pstats,sys; p=pstats.Stats(sys.argv[1]); p.sort_stats('tottime').print_stats(40); p.sort_stats('cumulative').print_stats(60)" \
         "$O/${TAG}_sim_c5r.prof" > "$O/${TAG}_sim_c5r_pstats.txt" 2>&1
       head -70 "$O/${TAG}_sim_c5r_pstats.txt" | tail -50 ;;
+    simtrace)
+      # rocprofv3 kernel trace of the c5 agent simulation, 4 iterations (are slow wall times GPU time?)
+      (cd /tmp && PYTHONPATH="$R" timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$O/${TAG}_simtrace" \
+        -o run -- python3 -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 4 --dropout 0.01 \
+        --latency deterministic -k -s 5 > "$O/${TAG}_simtrace.log" 2>&1) || { tail -30 "$O/${TAG}_simtrace.log"; exit 1; }
+      grep "iteration [0-9]*:" "$O/${TAG}_simtrace.log" ;;
+    ecstraus)
+      # the EC combine alone at one G = 8 rank's c5 share (D = 121, T = 20) with 1 / 2 / 4 terms per row chain,
+      # then one rank's shares -> final with the row kernel at each (tools/probes/rank8_overlap_probe.py --straus)
+      for g in 1 2 4; do
+        timeout -k 10 120 python tools/ec_bench.py --D 121 --T 20 --scalars lagrange --coop 2 --row-terms $g --reps 20 \
+          --cpu-sample 10 > "$O/${TAG}_ecbench_row$g.log" 2>&1 || { tail -20 "$O/${TAG}_ecbench_row$g.log"; exit 1; }
+        tail -1 "$O/${TAG}_ecbench_row$g.log" | cut -c1-300
+      done
+      timeout -k 10 300 python -u tools/probes/rank8_overlap_probe.py --straus > "$O/${TAG}_rank8_straus.log" 2>&1 \
+        || { tail -20 "$O/${TAG}_rank8_straus.log"; exit 1; }
+      grep -v amdgpu.ids "$O/${TAG}_rank8_straus.log" ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \
