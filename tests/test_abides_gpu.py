@@ -71,11 +71,17 @@ def test_simulation_on_a_device_group(monkeypatch, spec):
     protocol._group = None
 
 
-def test_simulation_c5_shape_reduced():
+@pytest.mark.parametrize("group", ["", "0,0,0,0"], ids=["one_gpu", "loopback4"])
+def test_simulation_c5_shape_reduced(monkeypatch, group):
     """BASELINE c5's client count and per-iteration 1 % dropouts (--dropout 0.01: PCG64(seed=t)
     choice per iteration) through the agents, with L = 2^16 and 2 iterations; deterministic latency,
-    so the offline sets are exactly the injected ones (41 per iteration)."""
+    so the offline sets are exactly the injected ones (41 per iteration).  loopback4: the server's
+    store and sums over a 4-rank device group on the one GPU (client-sharded rows, slot-sharded S,
+    the group's exchange) -- the drop-in server's multi-GPU form at c5's client count."""
     from flamingo_amd.abides.config_flamingo import offline_schedule, run
+    from flamingo_amd.abides.flamingo import protocol
+    if group:
+        monkeypatch.setenv("FLM_GROUP_DEVICES", group)
     res = run(["-c", "flamingo", "-n", "4096", "--vector_len", "65536", "-i", "2", "--dropout", "0.01", "-k",
                "-s", "5", "--latency", "deterministic"])
     srv = res["server"]
@@ -85,6 +91,11 @@ def test_simulation_c5_shape_reduced():
         assert srv.online_counts[it] == 4096 - sum(1 for its in sch.values() if it in its) == 4055
         assert np.all(out == 4055), it
         assert srv.pairs_per_iteration[it] > 500
+    if group:
+        assert srv._store.G == 4
+        srv._store.close()
+        protocol._group.close()
+        protocol._group = None
 
 
 def test_assigned_vec_sum_partial_on_the_gpu():
