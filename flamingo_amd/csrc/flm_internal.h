@@ -158,6 +158,14 @@ struct DeviceScope {
     DeviceScope(const DeviceScope &) = delete;
     DeviceScope &operator=(const DeviceScope &) = delete;
 };
+// Size of a scratch allocation that must hold `bytes`: half again as much, at most 64 MiB extra,
+// in whole 4 KiB pages.  Buffers sized by per-round counts (K seeds, D pairs) change by a few
+// percent from round to round; allocating exactly made every new maximum a hipFree + hipMalloc,
+// and hipFree waits for the whole device (4.8 ms inside the server's unmask, profiles/r05_hip_api_top.txt).
+inline size_t grow_bytes(size_t bytes) {
+    const size_t slack = bytes / 2 < (size_t(64) << 20) ? bytes / 2 : (size_t(64) << 20);
+    return (bytes + slack + 4095) & ~size_t(4095);
+}
 // Upload host rows and seeds and enqueue the fused round over mask window [mask_lo, mask_hi) into
 // d_out (L words) on the context's stream; returns without synchronising.
 int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,

@@ -36,8 +36,13 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
+        size_t want = flm::rt::grow_bytes(std::max<size_t>(bytes, 256));
         hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {  // no room for the slack: exactly what was asked
+            (void)hipGetLastError();
+            want = std::max<size_t>(bytes, 256);
+            e = hipMalloc(&p, want);
+        }
         if (e == hipSuccess) cap = want;
         return e;
     }

@@ -62,6 +62,12 @@ struct flm_store {
     hipEvent_t t0 = nullptr, t1 = nullptr;  // device time of the last partial sum (rank 0)
     hipEvent_t u0 = nullptr, u1 = nullptr;  // device time of the last unmask, uploads to D2H (rank 0)
     float unmask_ms = -1.0f;
+    // pinned bounce buffers of the host-facing calls (flm_store_unmask, flm_store_partial_host): the
+    // caller's seeds and output are pageable numpy memory, which HIP would stage or pin per call
+    uint8_t *hseeds = nullptr;   // K x 32 seeds + K signs
+    size_t hseeds_cap = 0;
+    uint32_t *hout = nullptr;    // L words: every rank's shard lands at its offset lo
+    bool bounce_busy = false;    // a call that failed after enqueueing may have left DMAs reading them
     std::string err;
 };
 
@@ -101,6 +107,18 @@ int grow_rows(flm_store *st, StoreRank &r, int want) {
     return 0;
 }
 
+// The pinned bounce buffers are free once every rank's stream has drained (only after a call that
+// returned an error between its enqueues and its synchronisation can they still be in use).
+int bounce_idle(flm_store *st) {
+    if (!st->bounce_busy) return 0;
+    for (StoreRank &k : st->rk) {
+        FLM_SHIP(st, hipSetDevice(k.device));
+        FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
+    }
+    st->bounce_busy = false;
+    return 0;
+}
+
 // Only the store's own objects are touched: the context or group may already be gone (a caller
 // that frees its group first).  Its own events cover every queued use of its buffers: uploads on
 // the copy stream, the partial sum (consumed, t1); flm_store_unmask is synchronous.
@@ -125,6 +143,8 @@ void release(flm_store *st) {
         if (r.consumed) (void)hipEventDestroy(r.consumed);
         if (r.copy) (void)hipStreamDestroy(r.copy);
     }
+    if (st->hseeds) (void)hipHostFree(st->hseeds);
+    if (st->hout) (void)hipHostFree(st->hout);
     if (st->t0) (void)hipEventDestroy(st->t0);
     if (st->t1) (void)hipEventDestroy(st->t1);
     if (st->u0) (void)hipEventDestroy(st->u0);
@@ -169,6 +189,13 @@ int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int 
         if (e == hipSuccess) e = hipEventCreateWithFlags(&k.consumed, hipEventDisableTiming);
         if (e == hipSuccess) e = hipMalloc(&k.S, st->S * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMalloc(&k.out, st->S * sizeof(uint32_t));
+        // the unmask's seeds + signs (33 B each): |U| + D seeds, D about a quarter of N at 1 %
+        // dropouts and neighbourhood ~22 (c5), so 2 N seeds now and grow_bytes' slack later
+        if (e == hipSuccess) {
+            k.seeds_cap = flm::rt::grow_bytes((size_t)std::max(1, capacity) * 2 * 33);
+            e = hipMalloc(&k.seeds, k.seeds_cap);
+            if (e != hipSuccess) k.seeds_cap = 0;
+        }
         for (int b = 0; b < kStoreRing && e == hipSuccess; ++b) {
             e = hipHostMalloc(&k.stage[b], L * sizeof(uint32_t), hipHostMallocDefault);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&k.stage_done[b], hipEventDisableTiming);
@@ -181,6 +208,8 @@ int flm_store_create(flm_store **out, flm_ctx *ctx, flm_group *g, size_t L, int 
         if (hipEventCreate(&st->t0) != hipSuccess || hipEventCreate(&st->t1) != hipSuccess ||
             hipEventCreate(&st->u0) != hipSuccess || hipEventCreate(&st->u1) != hipSuccess)
             rc = sfail(st, FLM_EHIP, "flm_store_create: hipEventCreate");
+        else if (hipHostMalloc(&st->hout, L * sizeof(uint32_t), hipHostMallocPortable) != hipSuccess)
+            rc = sfail(st, FLM_ENOMEM, "flm_store_create: pinned output buffer");
     }
     if (rc) {
         std::string m = st->err;
@@ -304,16 +333,20 @@ int flm_store_partial_host(flm_store *st, uint32_t *out) {
     flm::rt::DeviceScope dev_scope_;  // the caller's device comes back on return
     if (!st || !out) return sfail(st, FLM_EINVAL, "NULL argument");
     if (!st->have_partial) return sfail(st, FLM_EINVAL, "no partial sum enqueued");
+    if (int rc = bounce_idle(st)) return rc;
+    st->bounce_busy = true;
     for (StoreRank &k : st->rk) {
         if (k.hi <= k.lo) continue;
         FLM_SHIP(st, hipSetDevice(k.device));
-        FLM_SHIP(st, hipMemcpyAsync(out + k.lo, k.S, (k.hi - k.lo) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        FLM_SHIP(st, hipMemcpyAsync(st->hout + k.lo, k.S, (k.hi - k.lo) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                     flm::rt::stream_of(k.ctx)));
     }
     for (StoreRank &k : st->rk) {
         FLM_SHIP(st, hipSetDevice(k.device));
         FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
     }
+    st->bounce_busy = false;
+    std::memcpy(out, st->hout, st->L * sizeof(uint32_t));
     return 0;
 }
 
@@ -325,8 +358,22 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
         if (signs[k] != 1 && signs[k] != -1) return sfail(st, FLM_EINVAL, "signs must be +1 or -1");
     const size_t sb = (size_t)K * 33;
     st->unmask_ms = -1.0f;
+    if (int rc = bounce_idle(st)) return rc;
+    if (K > 0) {  // one pinned copy of seeds + signs, read by every rank's upload (idle: the last call synced)
+        if (st->hseeds_cap < sb) {
+            if (st->hseeds) (void)hipHostFree(st->hseeds);
+            st->hseeds = nullptr;
+            st->hseeds_cap = 0;
+            const size_t want = flm::rt::grow_bytes(sb);
+            FLM_SHIP(st, hipHostMalloc(&st->hseeds, want, hipHostMallocPortable));
+            st->hseeds_cap = want;
+        }
+        std::memcpy(st->hseeds, seeds, (size_t)K * 32);
+        std::memcpy(st->hseeds + (size_t)K * 32, signs, (size_t)K);
+    }
     FLM_SHIP(st, hipSetDevice(st->rk[0].device));
     FLM_SHIP(st, hipEventRecord(st->u0, flm::rt::stream_of(st->rk[0].ctx)));
+    st->bounce_busy = true;
     for (StoreRank &k : st->rk) {
         const size_t n = k.hi - k.lo;
         if (n == 0) continue;
@@ -334,22 +381,22 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
         hipStream_t s = flm::rt::stream_of(k.ctx);
         if (K > 0) {
             if (k.seeds_cap < sb) {
-                FLM_SHIP(st, hipStreamSynchronize(s));
+                if (k.seeds) FLM_SHIP(st, hipStreamSynchronize(s));  // the last unmask may still read it
                 if (k.seeds) (void)hipFree(k.seeds);
                 k.seeds = nullptr;
                 k.seeds_cap = 0;
-                FLM_SHIP(st, hipMalloc(&k.seeds, sb));
-                k.seeds_cap = sb;
+                const size_t want = flm::rt::grow_bytes(sb);  // K moves by a few % per iteration
+                FLM_SHIP(st, hipMalloc(&k.seeds, want));
+                k.seeds_cap = want;
             }
-            FLM_SHIP(st, hipMemcpyAsync(k.seeds, seeds, (size_t)K * 32, hipMemcpyHostToDevice, s));
-            FLM_SHIP(st, hipMemcpyAsync(k.seeds + (size_t)K * 32, signs, (size_t)K, hipMemcpyHostToDevice, s));
+            FLM_SHIP(st, hipMemcpyAsync(k.seeds, st->hseeds, sb, hipMemcpyHostToDevice, s));
         }
         // final[lo + l] = S[l] + sum_k sign_k PRG(seed_k)[lo + l], l < n: S as one row, PRG words lo..
         if (int rc = flm_aggregate_unmask_dev(k.ctx, k.S, st->S, 1, K ? k.seeds : nullptr,
                                               K ? reinterpret_cast<const int8_t *>(k.seeds + (size_t)K * 32) : nullptr,
                                               K, n, 0, n, k.lo, k.out, s))
             return sfail(st, rc, std::string("store unmask: ") + flm_last_error(k.ctx));
-        FLM_SHIP(st, hipMemcpyAsync(out + k.lo, k.out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        FLM_SHIP(st, hipMemcpyAsync(st->hout + k.lo, k.out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
     FLM_SHIP(st, hipSetDevice(st->rk[0].device));
     FLM_SHIP(st, hipEventRecord(st->u1, flm::rt::stream_of(st->rk[0].ctx)));
@@ -357,6 +404,8 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
         FLM_SHIP(st, hipSetDevice(k.device));
         FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
     }
+    st->bounce_busy = false;
+    std::memcpy(out, st->hout, st->L * sizeof(uint32_t));
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, st->u0, st->u1) == hipSuccess) st->unmask_ms = ms;
     return 0;
