@@ -8,6 +8,7 @@ wall time and the collector time inside it, and the run's collector totals per g
 
     python tools/probes/sim_gc_probe.py [--freeze] -- -n 4096 --vector_len 1048576 -i 10 --dropout 0.01 ...
 
+--threshold N: gc.set_threshold(N, 10, 10) (fewer young collections, so fewer full ones).
 --freeze: gc.freeze() when the Kernel starts its event loop (after the agents are built), so the
           full collections no longer walk the simulation's setup objects.
 """
@@ -26,6 +27,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--freeze", action="store_true")
+    ap.add_argument("--threshold", type=int, default=0, help="gc.set_threshold(N, 10, 10) before the run")
     ap.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     argv = [x for x in a.rest if x != "--"]
@@ -41,6 +43,8 @@ def main():
             collections.append((info["generation"], start.get("t", t), t - start.get("t", t)))
 
     gc.callbacks.append(cb)
+    if a.threshold:
+        gc.set_threshold(a.threshold, 10, 10)
 
     from flamingo_amd import ingest
     from flamingo_amd.abides import kernel as K
@@ -80,7 +84,7 @@ def main():
     for g, _, d in collections:
         n, tot, mx = per_gen.get(g, (0, 0.0, 0.0))
         per_gen[g] = (n + 1, tot + d, max(mx, d))
-    rec = {"freeze": a.freeze, "run_s": round(t_run, 2), "unmask_calls": rows,
+    rec = {"freeze": a.freeze, "threshold": gc.get_threshold(), "run_s": round(t_run, 2), "unmask_calls": rows,
            "gc": {str(g): {"count": n, "total_ms": round(tot * 1e3, 1), "max_ms": round(mx * 1e3, 3)}
                   for g, (n, tot, mx) in sorted(per_gen.items())}}
     print("[gc probe] " + json.dumps(rec), flush=True)
