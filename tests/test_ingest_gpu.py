@@ -143,3 +143,34 @@ def test_group_close_refused_while_a_store_is_open():
         grp.close()
     st.close()
     grp.close()
+
+
+@pytest.mark.parametrize("G", [1, 2])
+def test_store_unmask_seed_counts_grow_and_shrink(G):
+    """K from call to call past the store's first seed buffer (made for 2 x capacity seeds) and back
+    down: the device seed buffer and the pinned bounce buffers regrow (with slack) and stay exact; a
+    call refused for its signs leaves the store usable."""
+    from flamingo_amd import DeviceGroup, MaskEngine
+    from flamingo_amd.ingest import VectorStore
+    L, N = 5000, 4
+    eng = MaskEngine(0) if G == 1 else DeviceGroup([0] * G)
+    try:
+        st = VectorStore(eng, L, capacity=N)
+        rows, _, _ = _case(N, 0, L, 77)
+        for i in range(N):
+            st.add(i, rows[i])
+        st.partial_sum()
+        for j, K in enumerate([3, 200, 5000, 7, 6000]):
+            _, seeds, signs = _case(1, K, 1, 1000 + j)
+            if j == 3:
+                bad = signs.copy()
+                bad[0] = 0
+                with pytest.raises(RuntimeError, match="signs"):
+                    st.unmask(seeds, bad)
+            got = st.unmask(seeds, signs)
+            want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+            assert np.array_equal(got, want), (G, K)
+            assert np.array_equal(st.host_partial(), rows.sum(axis=0, dtype=np.uint64).astype(np.uint32))
+        st.close()
+    finally:
+        eng.close()
