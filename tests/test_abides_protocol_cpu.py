@@ -221,3 +221,22 @@ def test_protocol_per_iteration_dropouts_on_oracle(oracle_engine, capsys):
         assert n_off == 3 and srv.online_counts[it] <= 32 - n_off
         assert np.all(out == srv.online_counts[it]) and srv.pairs_per_iteration[it] > 0
     assert "final_sum == |U| in every slot: True" in capsys.readouterr().out
+
+
+def test_run_raises_the_gc_threshold_and_restores_it(monkeypatch):
+    """config_flamingo.run raises the young-generation threshold for the event loop only
+    (profiles/r05_sim_gc_threshold.log) and gives the caller's back, also when the run raises."""
+    import gc
+    from flamingo_amd.abides import config_flamingo as CF
+    before = gc.get_threshold()
+    seen = []
+
+    def fake_run(args):
+        seen.append(gc.get_threshold())
+        raise RuntimeError("stop")
+
+    monkeypatch.setattr(CF, "_run", fake_run)
+    with pytest.raises(RuntimeError, match="stop"):
+        CF.run(["-c", "flamingo", "-n", "8"])
+    assert seen and seen[0][0] >= CF.GC_THRESHOLD0
+    assert gc.get_threshold() == before
