@@ -56,6 +56,21 @@ def main():
                 rows.append([round(t_ec, 2), round(wall, 2), round(st.unmask_ms(), 2)])
             out[f"idle{idle}_ec{int(ec)}"] = rows
             print(f"idle {idle} s, EC before: {ec}:  [ec ms, unmask wall ms, unmask GPU ms] {rows}", flush=True)
+    # a new seed count K every call, as every simulation iteration has (|U| + D moves): a new launch
+    # plan (its work-item table allocated and uploaded) inside the unmask
+    for idle in (0.0, 0.5):
+        rows = []
+        for t in range(3 * trials):
+            time.sleep(idle)
+            Kt = K + 1 + t + int(idle * 100)
+            eng.ec_combine_wire(c1, shares, lams)
+            t0 = time.perf_counter()
+            st.unmask(seeds[:Kt] if Kt <= K else np.concatenate([seeds, seeds[:Kt - K]]),
+                      signs[:Kt] if Kt <= K else np.concatenate([signs, signs[:Kt - K]]))
+            wall = (time.perf_counter() - t0) * 1e3
+            rows.append([Kt, round(wall, 2), round(st.unmask_ms(), 2)])
+        out[f"new_K_idle{idle}"] = rows
+        print(f"a new K every call, idle {idle} s, EC before:  [K, unmask wall ms, unmask GPU ms] {rows}", flush=True)
     # the simulation's client traffic before each reconstruction: every client's y_i made on the
     # GPU and copied into a fresh pageable 4 MiB array (MaskEngine.client_mask, as sendVectors
     # does), handed to the store and dropped
