@@ -81,6 +81,11 @@ struct Plan {
     hipEvent_t ready = nullptr;
     hipStream_t up_stream = nullptr;
     bool ready_known = true;
+    // the plan's last launch (recorded by run_plan), and when it was last used: the cache recycles
+    // its least recently used plan's buffers once that launch has completed
+    hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    uint64_t last_use = 0;
 };
 
 // Pinned host + device staging for the small per-call tables the *_dev entry points upload
@@ -122,6 +127,7 @@ struct flm_ctx {
     hipEvent_t copy_done[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t copy_start = nullptr;
     std::map<PlanKey, Plan *> plans;
+    uint64_t plan_clock = 0;
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
     int table_k = -1;  // seeds in the current device seed table
     int tune_variant = -1;   // items_kernel variant, -1 = auto
@@ -429,9 +435,11 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items, hipStream_t 
 void plan_free(Plan *plan) {
     plan->items.release();
     if (plan->ready) (void)hipEventDestroy(plan->ready);
+    if (plan->done) (void)hipEventDestroy(plan->done);
     delete plan;
 }
 
+constexpr size_t kPlanCache = 64;        // launch plans kept per context (shapes)
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
 constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this many a whole-vector round is not split
 constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
@@ -568,17 +576,42 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
     PlanKey key{ctx->tune_subtiles + 100 * ctx->tune_pairing + 1000 * ctx->tune_min_items, pitch, (uint64_t)N,
                 (uint64_t)K, L, mask_lo, mask_hi, prg_slot0};
     auto f = ctx->plans.find(key);
-    if (f != ctx->plans.end()) { *rc = 0; return f->second; }
+    if (f != ctx->plans.end()) {
+        f->second->last_use = ++ctx->plan_clock;
+        *rc = 0;
+        return f->second;
+    }
+    // A full cache (kPlanCache shapes; a server whose seed count changes every round makes a new
+    // shape every round) hands its least recently used plan's item buffer and events to the new
+    // plan once that plan's last launch has completed -- no hipFree, which would wait for the
+    // whole device, and no hipMalloc while the buffer is big enough.
+    Plan *plan = nullptr;
+    if (ctx->plans.size() >= kPlanCache) {
+        auto lru = ctx->plans.begin();
+        for (auto it = ctx->plans.begin(); it != ctx->plans.end(); ++it)
+            if (it->second->last_use < lru->second->last_use) lru = it;
+        Plan *old = lru->second;
+        hipError_t e = old->done ? hipEventSynchronize(old->done) : hipSuccess;  // long done, as a rule
+        if (e == hipSuccess && old->ready) e = hipEventSynchronize(old->ready);
+        if (e != hipSuccess) {
+            *rc = fail(ctx, FLM_EHIP, "plan cache: waiting for a recycled plan failed: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+        ctx->plans.erase(lru);
+        plan = new Plan();
+        plan->items = old->items;  // the buffers move; the old Plan object goes
+        plan->ready = old->ready;
+        plan->done = old->done;
+        delete old;
+    } else {
+        plan = new Plan();
+    }
     std::vector<Item> items;
-    Plan *plan = new Plan();
     build_aggregate_items(ctx->tune_subtiles, ctx->tune_pairing, pitch, N, K, L, mask_lo, mask_hi, prg_slot0, items,
                           *plan, ctx->tune_min_items);
     *rc = upload_plan(ctx, *plan, items, s);
     if (*rc) { plan_free(plan); return nullptr; }
-    if (ctx->plans.size() > 64) {  // bound the cache (hipFree waits for the launches still reading them)
-        for (auto &kv : ctx->plans) plan_free(kv.second);
-        ctx->plans.clear();
-    }
+    plan->last_use = ++ctx->plan_clock;
     ctx->plans[key] = plan;
     return plan;
 }
@@ -650,6 +683,17 @@ int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, u
     const int variant_id = pick_variant(ctx, plan);
     FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
                                    ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
+    // `done` completes after every launch of the plan so far: the cache recycles its items only then.
+    // A launch on another stream than the last one first orders after that one's `done`.
+    if (!plan.done) {
+        FLM_HIP(ctx, hipEventCreateWithFlags(&plan.done, hipEventDisableTiming));
+    } else if (plan.done_stream != s) {
+        const hipError_t q = hipEventQuery(plan.done);
+        if (q == hipErrorNotReady) FLM_HIP(ctx, hipStreamWaitEvent(s, plan.done, 0));
+        else if (q != hipSuccess) FLM_HIP(ctx, q);
+    }
+    FLM_HIP(ctx, hipEventRecord(plan.done, s));
+    plan.done_stream = s;
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * plan.subtiles;
     ctx->last_atomics = plan.atomics;

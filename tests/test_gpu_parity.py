@@ -138,6 +138,22 @@ def test_aggregate_vs_oracle(eng, N, K, L):
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
 
 
+def test_plan_cache_recycles_past_its_capacity():
+    """More distinct round shapes than the launch-plan cache holds (64; a server's seed count changes
+    every iteration): the least recently used plan's buffers are recycled, never freed under a
+    launch, and every round -- new shapes, and shapes seen before and evicted -- stays exact."""
+    from flamingo_amd import MaskEngine
+    L, N = 4096, 2
+    with MaskEngine(0) as e:
+        e.set_tuning("small", 0)                     # the planned items_kernel path, not small_round_kernel
+        rows, seeds, signs = rand_case(4242, N, 90, L)
+        for K in list(range(1, 81)) + [1, 2, 3, 79, 80, 90]:
+            got = e.aggregate_unmask(list(rows), seeds[:K], signs[:K], L=L)
+            want = O.aggregate_unmask(rows, seeds[:K], signs[:K], L=L, threads=8)
+            assert np.array_equal(got, want), K
+            assert e.last_plan()["variant"] != 100   # not the small-round kernel
+
+
 def test_aggregate_wraps_mod_2_32(eng):
     rows = np.full((7, 333), 0xFFFFFFFF, np.uint32)
     out = eng.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8))
