@@ -154,6 +154,44 @@ def test_plan_cache_recycles_past_its_capacity():
             assert e.last_plan()["variant"] != 100   # not the small-round kernel
 
 
+def test_plan_cache_recycling_across_streams():
+    """One shape launched on two streams behind long queued work, then more new shapes (mask
+    windows of the same seeds, so the context's shared seed table stays valid, include/flamingo_hip.h)
+    than the cache holds, on a third stream, while those launches may still run: the recycled plan's
+    item buffer is reused only after every launch of it (its `done` event, the second stream's
+    launch ordered after the first's)."""
+    import torch
+    from flamingo_amd import MaskEngine
+    L, N, K = 4096, 2, 100
+    with MaskEngine(0) as e:
+        e.set_tuning("small", 0)
+        rows, seeds, signs = rand_case(5151, N, K, L)
+        d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+        d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+        sa, sb, sc = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        outs = []
+        for st in (sa, sb):
+            with torch.cuda.stream(st):
+                a = torch.randn(2048, 2048, device="cuda")
+                for _ in range(20):                   # queue work ahead of the launch
+                    a = a @ a / 2048.0
+                out = torch.empty(L, dtype=torch.int32, device="cuda")
+                e.aggregate_unmask_dev(d_rows, d_seeds, d_signs, out, L=L, stream=st)
+                outs.append(out)
+        with torch.cuda.stream(sc):
+            for j in range(1, 80):                    # 79 new shapes: recycles the plan of the two launches
+                last = torch.empty(L, dtype=torch.int32, device="cuda")
+                e.aggregate_unmask_dev(d_rows, d_seeds, d_signs, last, L=L, mask_lo=0, mask_hi=16 * j, stream=sc)
+        torch.cuda.synchronize()
+        want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+        for out in outs:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        hi = 16 * 79
+        got = last.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got[:hi], want[:hi])
+        assert np.array_equal(got[hi:], rows[:, hi:].sum(axis=0, dtype=np.uint64).astype(np.uint32))
+
+
 def test_aggregate_wraps_mod_2_32(eng):
     rows = np.full((7, 333), 0xFFFFFFFF, np.uint32)
     out = eng.aggregate_unmask(rows, np.zeros((0, 32), np.uint8), np.zeros(0, np.int8))
