@@ -81,10 +81,9 @@ struct Plan {
     hipEvent_t ready = nullptr;
     hipStream_t up_stream = nullptr;
     bool ready_known = true;
-    // the plan's last launch (recorded by run_plan), and when it was last used: the cache recycles
-    // its least recently used plan's buffers once that launch has completed
-    hipEvent_t done = nullptr;
-    hipStream_t done_stream = nullptr;
+    // the plan's last launch on each stream it ran on (recorded by run_plan), and when it was last
+    // used: the cache recycles its least recently used plan's buffers once those have completed
+    std::vector<std::pair<hipStream_t, hipEvent_t>> done;
     uint64_t last_use = 0;
 };
 
@@ -435,11 +434,14 @@ int upload_plan(flm_ctx *ctx, Plan &plan, std::vector<Item> &items, hipStream_t 
 void plan_free(Plan *plan) {
     plan->items.release();
     if (plan->ready) (void)hipEventDestroy(plan->ready);
-    if (plan->done) (void)hipEventDestroy(plan->done);
+    for (auto &d : plan->done) (void)hipEventDestroy(d.second);
     delete plan;
 }
 
 constexpr size_t kPlanCache = 64;        // launch plans kept per context (shapes)
+#ifndef FLM_PLAN_DONE_EVENTS
+#define FLM_PLAN_DONE_EVENTS 1  // 0: A/B builds only (recycling then has no completion to wait for)
+#endif
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
 constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this many a whole-vector round is not split
 constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
@@ -591,7 +593,9 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
         for (auto it = ctx->plans.begin(); it != ctx->plans.end(); ++it)
             if (it->second->last_use < lru->second->last_use) lru = it;
         Plan *old = lru->second;
-        hipError_t e = old->done ? hipEventSynchronize(old->done) : hipSuccess;  // long done, as a rule
+        hipError_t e = hipSuccess;
+        for (auto &d : old->done)  // long done, as a rule
+            if (e == hipSuccess) e = hipEventSynchronize(d.second);
         if (e == hipSuccess && old->ready) e = hipEventSynchronize(old->ready);
         if (e != hipSuccess) {
             *rc = fail(ctx, FLM_EHIP, "plan cache: waiting for a recycled plan failed: %s", hipGetErrorString(e));
@@ -601,7 +605,7 @@ Plan *aggregate_plan(flm_ctx *ctx, uint64_t pitch, int N, int K, uint64_t L, uin
         plan = new Plan();
         plan->items = old->items;  // the buffers move; the old Plan object goes
         plan->ready = old->ready;
-        plan->done = old->done;
+        plan->done.swap(old->done);  // (stream, event) pairs: the events are reused per stream
         delete old;
     } else {
         plan = new Plan();
@@ -683,17 +687,29 @@ int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, u
     const int variant_id = pick_variant(ctx, plan);
     FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
                                    ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
-    // `done` completes after every launch of the plan so far: the cache recycles its items only then.
-    // A launch on another stream than the last one first orders after that one's `done`.
-    if (!plan.done) {
-        FLM_HIP(ctx, hipEventCreateWithFlags(&plan.done, hipEventDisableTiming));
-    } else if (plan.done_stream != s) {
-        const hipError_t q = hipEventQuery(plan.done);
-        if (q == hipErrorNotReady) FLM_HIP(ctx, hipStreamWaitEvent(s, plan.done, 0));
-        else if (q != hipSuccess) FLM_HIP(ctx, q);
+#if FLM_PLAN_DONE_EVENTS
+    // one event per stream the plan ran on, after its last launch there: the cache recycles the
+    // items only once all of them have completed (no dependency is added between the streams)
+    hipEvent_t *ev = nullptr;
+    for (auto &d : plan.done)
+        if (d.first == s) ev = &d.second;
+    if (!ev) {
+        if (plan.done.size() >= 8) {  // many streams over time: drop the entries already completed
+            std::vector<std::pair<hipStream_t, hipEvent_t>> keep;
+            for (auto &d : plan.done) {
+                if (hipEventQuery(d.second) == hipSuccess) (void)hipEventDestroy(d.second);
+                else keep.push_back(d);
+            }
+            (void)hipGetLastError();  // hipErrorNotReady from the queries
+            plan.done.swap(keep);
+        }
+        hipEvent_t e = nullptr;
+        FLM_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        plan.done.emplace_back(s, e);
+        ev = &plan.done.back().second;
     }
-    FLM_HIP(ctx, hipEventRecord(plan.done, s));
-    plan.done_stream = s;
+    FLM_HIP(ctx, hipEventRecord(*ev, s));
+#endif
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * plan.subtiles;
     ctx->last_atomics = plan.atomics;
