@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-copy", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-variants", action="store_true", help="skip the pairs-only variant")
+    ap.add_argument("--no-prg-expand", action="store_true", help="skip the standalone mask-expansion leg")
     ap.add_argument("--profile", action="store_true", help="minimal run for rocprofv3 (no CPU/copy legs)")
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (c2, c3, c5)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -460,6 +461,11 @@ def main():
         pk = practical_peak(eng, torch, rows_on, L, stream)
         res["roofline"]["practical_peak"] = pk
         res["roofline"]["frac_of_practical_peak"] = round(ach_gbs / pk["GB/s"], 4)
+    if G > 1:
+        res["scaling_check"] = scaling_check(G, strong, N, L, k_all, value, bytes_round,
+                                             eng.comm_size()[0] if rnd.comm == "rccl" else None, rnd.comm)
+    if rank == 0 and G == 1 and not args.profile and not args.no_prg_expand:
+        res["prg_expand"] = measure_prg_expand(eng, torch, stream, res["roofline_valu"].get("measured_chacha_ceiling_gwords"))
     if not args.profile and not args.no_variants:
         # every rank at once (each over its own rows and its own slot shard), rank 0 reports
         po = variant_pairs_only(eng, torch, rows_on, nbrs, N, L, stream, P, rnd.lo, rnd.hi)["pairs_only"]
@@ -926,7 +932,9 @@ def measure_h2c(eng, torch, reps=5, cpu_sample=4096):
            "table_sha256": hashlib.sha256(table.tobytes()).hexdigest()}
     try:
         with open(os.path.join(ROOT, "tests", "golden", "h2c_golden.json")) as f:
-            res["matches_reference_table"] = json.load(f)["table_sha256"] == res["table_sha256"]
+            gold = json.load(f)
+        res["matches_reference_table"] = gold["table_sha256"] == res["table_sha256"]
+        res["parity"] = gold.get("parity")
     except OSError:
         res["matches_reference_table"] = None
     # cpu_baseline leg: the oracle restatement (checker only, outside the GPU timing)
@@ -1022,6 +1030,80 @@ def mask_only_ceiling(eng, torch, d_seeds, d_signs, L, lo, hi, stream, reps=10):
     words = float(K) * (hi - lo)
     return {"what": "mask-only launch of the same K seeds over the same slot window (no rows), same run",
             "kernel_ms": round(ms, 4), "mask_gwords_per_s": round(words / (ms * 1e-3) / 1e9, 1)}
+
+
+PRG_EXPAND_K = 962  # the c5 round's dropout pairs D (bench other_configs.c5.dropout_pairs_D_mean, round 5)
+
+
+def measure_prg_expand(eng, torch, stream, ceil_gwords=None, K=PRG_EXPAND_K, L=1 << 20, reps=5):
+    """north_star (i) on its own: expand K recovered pair seeds into K masks of L slots in device
+    memory, one seed per row (flm_prg_expand_dev; the cancel_vec idiom of SA_ServiceAgent.py:596-603
+    for the whole batch of dropout pairs), outside the headline's timed loop.  Median of `reps`
+    launches on the bench stream.  Reports the bytes written against HBM peak and the mask words
+    per second against the same run's ChaCha ceiling (mask_only_ceiling: the summing kernel's
+    words/s with no rows), and checks the first and last 4096 slots of three rows against
+    oracle.prg (checker only)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # checker only
+    dev = torch.device("cuda", torch.cuda.current_device())
+    seeds = np.random.Generator(np.random.PCG64(962)).integers(0, 256, (K, 32), dtype=np.uint8)
+    d_seeds = torch.from_numpy(seeds).to(dev)
+    out = torch.empty((K, L), dtype=torch.int32, device=dev)
+    for _ in range(2):
+        eng.prg_expand_dev(d_seeds, out, L, stream=stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(stream)
+    for i in range(reps):
+        eng.prg_expand_dev(d_seeds, out, L, stream=stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    times = [ev[i].elapsed_time(ev[i + 1]) for i in range(reps)]
+    ms = float(np.median(times))
+    plan = eng.last_plan()
+    n = 4096
+    ok = True
+    for k in (0, K // 2, K - 1):
+        for a in (0, L - n):
+            got = out[k, a:a + n].cpu().numpy().view(np.uint32)
+            ok &= bool(np.array_equal(got, O.prg(seeds[k].tobytes(), n, a)))
+    words = float(K) * L
+    gbs = 4.0 * words / (ms * 1e-3) / 1e9
+    gw = words / (ms * 1e-3) / 1e9
+    res = {"what": f"flm_prg_expand_dev: {K} pair seeds (c5's D) x L = {L} slots into device memory, one mask "
+                   f"row per seed, median of {reps} launches (SA_ServiceAgent.py:596-603)",
+           "K": K, "L": L, "kernel": "items_kernel<16> (one wave per 1024 slots of one seed)",
+           "items": plan["items"], "kernel_ms": round(ms, 4), "kernel_ms_all": [round(t, 4) for t in times],
+           "bytes_written_per_launch": int(4 * words), "GB/s_written": round(gbs, 1),
+           "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "mask_gwords_per_s": round(gw, 1),
+           "checked_against_oracle": {"match": ok, "rows": [0, K // 2, K - 1], "windows": [[0, n], [L - n, n]]}}
+    if ceil_gwords:
+        res["chacha_ceiling_gwords"] = ceil_gwords
+        res["frac_of_same_run_chacha_ceiling"] = round(gw / ceil_gwords, 4)
+    del out
+    torch.cuda.empty_cache()
+    return res
+
+
+# strong-scaled c4 (N = 1024, L = 2^20): one rank's shard kernel timed alone on one GPU with that rank's
+# exact shapes (DESIGN.md section 7; G = 1 is the round-5 driver bench), the prediction a SCALE line is read against
+SCALING_MODEL_RANK_MS = {1: 1.31, 2: 0.69, 4: 0.35, 8: 0.184}
+
+
+def scaling_check(G, strong, N, L, kernel_ms_per_rank, value_gbs, bytes_round, rccl_ranks, comm):
+    """What a multi-GPU line must show for its scaling to be read: the exchange
+    through the library's RCCL communicator with G ranks, and each rank's kernel against the
+    one-GPU model.  Pure host arithmetic (tested on the CPU, tests/test_bench_cpu.py)."""
+    pred = SCALING_MODEL_RANK_MS.get(G) if strong and N == 1024 and L == 1 << 20 else None
+    kmax = max(kernel_ms_per_rank)
+    res = {"model_source": "DESIGN.md section 7 (one rank's shard kernel timed alone on one GPU)",
+           "rccl_comm_ranks": rccl_ranks, "rccl_ranks_ok": bool(comm == "rccl" and rccl_ranks == G),
+           "predicted_rank_kernel_ms": pred, "measured_rank_kernel_ms_max": round(kmax, 4),
+           "predicted_value_gbs": None, "predicted_vs_measured": None}
+    if pred is not None:
+        pv = bytes_round / (pred * 1e-3) / 1e9
+        res["predicted_value_gbs"] = round(pv, 1)
+        res["predicted_vs_measured"] = {"rank_kernel_ms": round(kmax / pred, 4), "value": round(value_gbs / pv, 4)}
+    return res
 
 
 # the fastest rows-only stream configuration measured (DESIGN.md section 8: merged accumulator, 4 rows in

@@ -43,6 +43,7 @@ SIGNATURES = {
     "flm_last_plan": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int),
                              ctypes.POINTER(_int)]),
     "flm_set_tuning": (_int, [_vp, ctypes.c_char_p, _int]),
+    "flm_get_tuning": (_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_int)]),
     "flm_plan_aggregate": (_int, [_int, _int, _sz, _int, _int, _sz, _sz, _sz, _u64, _vp, _int,
                                   ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "flm_ec_combine": (_int, [_vp, _u8p, _u8p, _u8p, _int, _int, _int, _u8p, _u8p, _u32p]),

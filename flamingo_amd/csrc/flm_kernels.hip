@@ -53,32 +53,15 @@ namespace flm {
 //   one statement, s_nop 0 after every rotate (and after every group)                            1.297
 //   one statement, s_nop 1 after each of the first three rotates, s_nop 2 after the fourth,
 //   nothing between the adds and xors (FLM_GAP_* defaults below)                                 1.176
-// Gaps between simple ops cost time; gaps after rotates buy it.  The gap macros stay
-// overridable (-DFLM_GAP_...) for tools/ab/build_variants.sh.
-#ifndef FLM_GAP_A1
+// Gaps between simple ops cost time; gaps after rotates buy it.
 #define FLM_GAP_A1 ""  // between the 2nd and 3rd add of a step
-#endif
-#ifndef FLM_GAP_AX
 #define FLM_GAP_AX ""  // adds -> xors
-#endif
-#ifndef FLM_GAP_X1
 #define FLM_GAP_X1 ""  // between the 2nd and 3rd xor
-#endif
-#ifndef FLM_GAP_XR
 #define FLM_GAP_XR ""  // xors -> rotates
-#endif
-#ifndef FLM_GAP_R0
 #define FLM_GAP_R0 "s_nop 1\n\t"  // after the 1st rotate
-#endif
-#ifndef FLM_GAP_R1
 #define FLM_GAP_R1 "s_nop 1\n\t"  // after the 2nd rotate
-#endif
-#ifndef FLM_GAP_R2
 #define FLM_GAP_R2 "s_nop 1\n\t"  // after the 3rd rotate
-#endif
-#ifndef FLM_GAP_RA
 #define FLM_GAP_RA "s_nop 2\n\t"  // after the 4th rotate, before the adds that read them
-#endif
 #define FLM_S_A(a, b) "v_add_u32 %[" #a "], %[" #b "], %[" #a "]\n\t"
 #define FLM_S_X(a, b) "v_xor_b32 %[" #a "], %[" #b "], %[" #a "]\n\t"
 #define FLM_S_R(a, s) "v_alignbit_b32 %[" #a "], %[" #a "], %[" #a "], " #s "\n\t"  // rotl(a, 32 - s)
@@ -200,25 +183,11 @@ __device__ __forceinline__ void chacha_mask_add(const SeedRec *__restrict__ rec,
     // (profiles/r02_ab_round1.log)
     FLM_QR4(x0, x5, x10, x15, x1, x6, x11, x12, x2, x7, x8, x13, x3, x4, x9, x14);
     // rounds 2..10
-#ifdef FLM_COMPILER_QR
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-        FLM_QR(x0, x4, x8, x12);
-        FLM_QR(x1, x5, x9, x13);
-        FLM_QR(x2, x6, x10, x14);
-        FLM_QR(x3, x7, x11, x15);
-        FLM_QR(x0, x5, x10, x15);
-        FLM_QR(x1, x6, x11, x12);
-        FLM_QR(x2, x7, x8, x13);
-        FLM_QR(x3, x4, x9, x14);
-    }
-#else
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
         FLM_QR4(x0, x4, x8, x12, x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15);
         FLM_QR4(x0, x5, x10, x15, x1, x6, x11, x12, x2, x7, x8, x13, x3, x4, x9, x14);
     }
-#endif
     // feed-forward (input words 13..15 are zero), fold "abcd"/sign, accumulate
     m[0] += (x0 + kSigma0) ^ xc;
     m[1] += (x1 + kSigma1) ^ xc;
@@ -291,25 +260,6 @@ __device__ __forceinline__ void reduce_out(const u32x4 *__restrict__ lds, uint32
 }
 
 // --------------------------------------------------------------- main kernel
-#ifdef FLM_STATIC_UNITS
-constexpr bool kClaimUnits = false;  // probe build: the static split of rows and seeds over the waves
-#else
-constexpr bool kClaimUnits = true;
-#endif
-#ifdef FLM_WG_TRACE
-// probe build only: per workgroup of items_kernel, [start, seeds done, end] in s_memrealtime ticks
-// (100 MHz) and the hardware ids (HW_ID | XCC_ID << 32), read back by flm_debug_wg_trace
-__device__ uint64_t flm_wg_trace[4 * 65536];
-#define FLM_WG_MARK(slot)                                                                          \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) {                                                  \
-        flm_wg_trace[4 * blockIdx.x + (slot)] = __builtin_amdgcn_s_memrealtime();                  \
-        if ((slot) == 0)                                                                           \
-            flm_wg_trace[4 * blockIdx.x + 3] = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) |       \
-                                               ((uint64_t)__builtin_amdgcn_s_getreg(0x7814) << 32); \
-    }
-#else
-#define FLM_WG_MARK(slot)
-#endif
 // One workgroup = one Item.  Wave w works on sub-tile s = w % S with chunk
 // c = w / S of the item's rows and seeds (Cw = 16 / S chunks).
 //   BL      rows are loaded in block layout (lane t: slots 16t..16t+15), the
@@ -331,12 +281,11 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
     __shared__ u32x4 lds[kWavesPerGroup * 256];  // 64 KiB: one 4 KiB region per wave
     __shared__ uint32_t claim[S];                 // next unclaimed unit of each sub-tile
 
-    FLM_WG_MARK(0);
     const Item it = items[blockIdx.x];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int s = w % S, c = w / S;
-    if constexpr (kClaimUnits && !SPREAD && Cw > 1) {
+    if constexpr (!SPREAD && Cw > 1) {
         if (threadIdx.x < S) claim[threadIdx.x] = 0u;
         __syncthreads();
     }
@@ -400,7 +349,7 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
             chacha_mask_add(rec, ctr, m);
             ++rec;
         }
-    } else if constexpr (kClaimUnits && Cw > 1) {
+    } else if constexpr (Cw > 1) {
         // Units claimed from a per-sub-tile LDS counter: unit i = seed i of the item, plus row i
         // when there is one.  With a static split (64 seeds per wave at c4) the SIMD's arbiter
         // lets some waves run far ahead, and a workgroup waited at its barrier for its slowest
@@ -486,7 +435,6 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         }
     }
 
-    FLM_WG_MARK(1);
     // ---- combine through this wave's LDS region (natural slot order), then
     // sum the Cw chunk partials of every sub-tile and write the tile.
     u32x4 *R = lds + w * 256;
@@ -501,7 +449,6 @@ __global__ __launch_bounds__(kThreads, WPE) void items_kernel(const Item *__rest
         const int valid = has_mask ? (int)it.mask_valid : (int)it.row_valid;
         const uint32_t bias = (has_rows ? it.row_bias : 0u) + (has_mask ? mbias : 0u);
         reduce_out<S>(lds, out, base, valid, bias, (flags & (kRowAtomic | kMaskAtomic)) != 0);
-        FLM_WG_MARK(2);
     } else {
         const bool same = flags & kSameTile;
         u32x4 mq[4];
@@ -895,11 +842,6 @@ hipError_t launch_seed_schedule(const uint8_t *d_seeds, const int8_t *d_signs, i
     return hipGetLastError();
 }
 
-// cache-policy bits of the production (merged) variant's row loads; overridable for A/B builds
-// (gfx950 buffer cpol: 1 = sc0, 2 = nt, 16 = sc1)
-#ifndef FLM_ROW_AUX
-#define FLM_ROW_AUX 0
-#endif
 template <int S, bool BL, bool MERGED, int WPE, int RUM = 2, int AUX = 0, bool SPREAD = false>
 static void launch_items_t(const Item *d_items, int n_items, const uint32_t *d_rows, uint64_t row_pitch,
                            const SeedRec *d_recs, const uint32_t *d_meta, uint32_t *d_out, hipStream_t stream) {
@@ -917,7 +859,7 @@ hipError_t launch_items(int subtiles, int variant, const Item *d_items, int n_it
     switch (variant) {                                               \
         case kVarCoalesced: FLM_L(S, false, false, 4); break;        \
         case kVarBlock: FLM_L(S, true, false, 4); break;             \
-        case kVarMerged: FLM_L(S, true, true, 4, 2, FLM_ROW_AUX); break; \
+        case kVarMerged: FLM_L(S, true, true, 4, 2, 0); break;           \
         case kVarMergedW8: FLM_L(S, true, true, 8); break;           \
         case kVarMergedRU4: FLM_L(S, true, true, 4, 4, 0); break;    \
         case kVarMergedNT: FLM_L(S, true, true, 4, 2, 2); break;     \
@@ -1022,9 +964,3 @@ hipError_t launch_chacha20_xor(const uint32_t key[8], const uint32_t nonce[2], u
 
 }  // namespace flm
 
-#ifdef FLM_WG_TRACE
-extern "C" int flm_debug_wg_trace(uint64_t *host, int n_items) {
-    const size_t n = (size_t)(n_items < 65536 ? n_items : 65536) * 4 * sizeof(uint64_t);
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(flm::flm_wg_trace), n, 0, hipMemcpyDeviceToHost);
-}
-#endif

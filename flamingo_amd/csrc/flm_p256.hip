@@ -294,52 +294,7 @@ __device__ __forceinline__ Fe from_mont(const Fe &a) {
     return fe_mul(a, one);
 }
 
-// FLM_INV_BINGCD (default 1): ec_finish inverts by binary GCD (fe_inv_bingcd below); 0 builds
-// Fermat's a^(p-2) for A/B runs
-#ifndef FLM_INV_BINGCD
-#define FLM_INV_BINGCD 1
-#endif
-#if !FLM_INV_BINGCD
-// a^(p-2): p-2 = ffffffff 00000001 00000000 00000000 00000000 ffffffff ffffffff fffffffd
-__device__ Fe fe_inv(const Fe &a) {
-    // x_k = a^(2^k - 1)
-    Fe x2 = fe_mul(fe_sqr(a), a);
-    Fe x4 = x2;
-    for (int i = 0; i < 2; ++i) x4 = fe_sqr(x4);
-    x4 = fe_mul(x4, x2);
-    Fe x8 = x4;
-    for (int i = 0; i < 4; ++i) x8 = fe_sqr(x8);
-    x8 = fe_mul(x8, x4);
-    Fe x16 = x8;
-    for (int i = 0; i < 8; ++i) x16 = fe_sqr(x16);
-    x16 = fe_mul(x16, x8);
-    Fe x32 = x16;
-    for (int i = 0; i < 16; ++i) x32 = fe_sqr(x32);
-    x32 = fe_mul(x32, x16);
-    // top 32 bits ffffffff, then 00000001
-    Fe r = x32;
-    for (int i = 0; i < 32; ++i) r = fe_sqr(r);
-    r = fe_mul(r, a);                       // ...00000001
-    for (int i = 0; i < 128; ++i) r = fe_sqr(r);  // three zero words + one more shift below
-    r = fe_mul(r, x32);                     // ffffffff
-    for (int i = 0; i < 32; ++i) r = fe_sqr(r);
-    r = fe_mul(r, x32);                     // ffffffff
-    // last word fffffffd = 30 ones, 0, 1
-    for (int i = 0; i < 16; ++i) r = fe_sqr(r);
-    r = fe_mul(r, x16);
-    Fe x14 = x8;                            // 2^14 - 1 = x8 shifted 6 + x4 (2 bits) ... build 14 ones
-    for (int i = 0; i < 4; ++i) x14 = fe_sqr(x14);
-    x14 = fe_mul(x14, x4);                  // 12 ones
-    x14 = fe_sqr(fe_sqr(x14));
-    x14 = fe_mul(x14, x2);                  // 14 ones
-    for (int i = 0; i < 14; ++i) r = fe_sqr(r);
-    r = fe_mul(r, x14);                     // 30 ones
-    r = fe_sqr(r);                          // 0
-    r = fe_sqr(r);
-    r = fe_mul(r, a);                       // 1
-    return r;
-}
-#endif  // !FLM_INV_BINGCD
+// ec_finish inverts by binary GCD (fe_inv_bingcd below), not Fermat's a^(p-2) (round 3)
 
 // ---- inversion by binary GCD (ec_finish_kernel's one-lane chain)
 // Pornin, "Optimized Binary GCD for Modular Inversion" (eprint 2020/972), Algorithm 2, with
@@ -869,14 +824,7 @@ __global__ __launch_bounds__(kEcThreads) void ec_mul_straus_kernel(const uint8_t
 // reconstruction) the per-lane kernel issues fewer instructions.  Exceptional cases as jac_add.
 constexpr int kCoopWaves = 4;
 constexpr int kCoopSlots = 11;
-// FLM_COOP_MODJ (default 1): the kernel carries W = Z^4 (coop_dbl_w / coop_add_w below); 0 builds the
-// plain Jacobian coop_dbl / coop_add for A/B runs
-#ifndef FLM_COOP_MODJ
-#define FLM_COOP_MODJ 1
-#endif
-#ifndef FLM_COOP_PRIO
-#define FLM_COOP_PRIO 1  // s_setprio(3) in ec_mul_coop_kernel (0: A/B builds)
-#endif
+// The cooperative kernels carry W = Z^4 (modified Jacobian, coop_dbl_w / coop_add_w below).
 
 // lane-major slots: a lane's 8 words are 32 contiguous bytes, moved with two 16-byte LDS ops
 // (0.5-1 % faster than word-major single-dword ops, profiles/r02_ab_coop_b128.log)
@@ -894,180 +842,8 @@ __device__ __forceinline__ Fe xget(const uint32_t *slot, int lane) {
     return a;
 }
 
-#if !FLM_COOP_MODJ
-// acc = 2 acc in every wave (all four waves hold acc; wave-uniform branches on w).  The additions
-// of the formula sit off wave 0's last level: L2 gives w1 the multiples of beta, w2 those of
-// gamma^2 and w3 the new Z, so L3 is alpha^2 and alpha (4 beta - X3) with four subtractions.
-// Slots: L1 writes 0..2 and the result lands in 6..8, so the next operation's first level (slots
-// 0..2) never overwrites what a wave is still reading.
-__device__ __forceinline__ void coop_dbl(Jac &acc, int w, int lane, uint32_t *S) {
-    Fe alpha;
-    if (w == 0) {
-        xput(S + 0 * 512, fe_sqr(acc.Z), lane);              // delta
-    } else if (w == 1) {
-        xput(S + 1 * 512, fe_sqr(acc.Y), lane);              // gamma
-    } else if (w == 2) {
-        xput(S + 2 * 512, fe_sqr(fe_add(acc.Y, acc.Z)), lane);  // (Y+Z)^2
-    }
-    __syncthreads();
-    if (w == 0) {
-        const Fe d = xget(S + 0 * 512, lane);
-        const Fe t = fe_mul(fe_sub(acc.X, d), fe_add(acc.X, d));
-        alpha = fe_add(fe_add(t, t), t);
-    } else if (w == 1) {
-        const Fe beta = fe_mul(acc.X, xget(S + 1 * 512, lane));
-        const Fe beta2 = fe_add(beta, beta);
-        const Fe beta4 = fe_add(beta2, beta2);
-        xput(S + 3 * 512, beta4, lane);
-        xput(S + 4 * 512, fe_add(beta4, beta4), lane);       // 8 beta
-    } else if (w == 2) {
-        const Fe g = xget(S + 1 * 512, lane);
-        Fe g8 = fe_sqr(g);
-        g8 = fe_add(g8, g8);
-        g8 = fe_add(g8, g8);
-        xput(S + 5 * 512, fe_add(g8, g8), lane);             // 8 gamma^2
-    } else {
-        const Fe d = xget(S + 0 * 512, lane), g = xget(S + 1 * 512, lane), sq = xget(S + 2 * 512, lane);
-        xput(S + 6 * 512, fe_sub(fe_sub(sq, g), d), lane);   // Z3
-    }
-    __syncthreads();
-    if (w == 0) {
-        const Fe x3 = fe_sub(fe_sqr(alpha), xget(S + 4 * 512, lane));
-        xput(S + 7 * 512, x3, lane);
-        xput(S + 8 * 512, fe_sub(fe_mul(alpha, fe_sub(xget(S + 3 * 512, lane), x3)), xget(S + 5 * 512, lane)), lane);
-    }
-    __syncthreads();
-    acc.X = xget(S + 7 * 512, lane);
-    acc.Y = xget(S + 8 * 512, lane);
-    acc.Z = xget(S + 6 * 512, lane);
-}
 
-// acc = sel ? acc + Q : acc (add-2007-bl, Q read from the LDS table) with the field
-// multiplications spread over the four waves:
-//   L1  w0: z1z1 = Z1^2   w1: z2z2 = Z2^2   w2: zz = (Z1+Z2)^2   w3: s1' = Y1 Z2
-//   L2  w0: u2 = X2 z1z1  w1: u1 = X1 z2z2  w2: Z3' = zz - z1z1 - z2z2, s2' = Y2 Z1   w3: s1 = s1' z2z2
-//   L3  w0: h = u2 - u1, i = (2h)^2          w2: s2 = s2' z1z1          w3: Z3 = Z3' h
-//   L4  w0: j = h i       w1: v = u1 i, 2v   w2: r = 2 (s2 - s1), r^2
-//   L5  w0: X3 = r^2 - j - 2v, r (v - X3)    w1: 2 s1 j
-//   L6  w0: Y3 = r (v - X3) - 2 s1 j, the exceptional cases (acc or Q at infinity, acc == +-Q)
-// 5 multiplications of latency instead of 16, one per level (s2' waits for L2, where w2 has room).  Slots (512 words each): A0 B1 C2 D3 E4 F5 G6 H7 I8
-// J9 K10; the result goes to D (X), E (Y), F (Z).
-__device__ __forceinline__ void coop_add(Jac &acc, bool sel, int tab_idx, bool neg, int w, int lane, uint32_t *S,
-                                         const uint32_t *tab) {
-    const uint32_t *q = tab + (size_t)tab_idx * 24 * 64;
-    Jac Q;
-    Q.X = xget(q, lane);
-    Q.Y = xget(q + 8 * 64, lane);
-    Q.Z = xget(q + 16 * 64, lane);
-    if (neg) Q.Y = fe_neg(Q.Y);
-    uint32_t *A = S, *B = S + 512, *C = S + 2 * 512, *Dd = S + 3 * 512, *E = S + 4 * 512, *F = S + 5 * 512,
-             *G = S + 6 * 512, *H = S + 7 * 512, *I = S + 8 * 512, *J = S + 9 * 512, *K = S + 10 * 512;
-    Fe z1z1, z2z2, zz, s2a, s1a, u1, u2, s2, s1, h, i, j, v, x3, y3a;
-    // L1
-    if (w == 0) {
-        z1z1 = fe_sqr(acc.Z);
-        xput(A, z1z1, lane);
-    } else if (w == 1) {
-        z2z2 = fe_sqr(Q.Z);
-        xput(B, z2z2, lane);
-    } else if (w == 2) {
-        zz = fe_sqr(fe_add(acc.Z, Q.Z));
-    } else {
-        s1a = fe_mul(acc.Y, Q.Z);
-    }
-    __syncthreads();
-    // L2
-    if (w == 0) {
-        xput(Dd, fe_mul(Q.X, z1z1), lane);  // u2
-    } else if (w == 1) {
-        u1 = fe_mul(acc.X, z2z2);
-        xput(E, u1, lane);
-    } else if (w == 2) {
-        z1z1 = xget(A, lane);
-        z2z2 = xget(B, lane);
-        xput(F, fe_sub(fe_sub(zz, z1z1), z2z2), lane);  // Z3'
-        s2a = fe_mul(Q.Y, acc.Z);
-    } else {
-        z2z2 = xget(B, lane);
-        xput(G, fe_mul(s1a, z2z2), lane);  // s1
-    }
-    __syncthreads();
-    // L3
-    if (w == 0) {
-        u2 = xget(Dd, lane);
-        u1 = xget(E, lane);
-        h = fe_sub(u2, u1);
-        const Fe h2 = fe_add(h, h);
-        i = fe_sqr(h2);
-        xput(H, i, lane);
-    } else if (w == 2) {
-        s2 = fe_mul(s2a, z1z1);
-    } else if (w == 3) {
-        u2 = xget(Dd, lane);
-        u1 = xget(E, lane);
-        xput(I, fe_mul(xget(F, lane), fe_sub(u2, u1)), lane);  // Z3 = Z3' h
-    }
-    __syncthreads();
-    // L4
-    if (w == 0) {
-        j = fe_mul(h, i);
-        xput(J, j, lane);
-    } else if (w == 1) {
-        i = xget(H, lane);
-        v = fe_mul(u1, i);
-        xput(K, v, lane);
-        xput(Dd, fe_add(v, v), lane);  // 2v (Dd's u2 was read at L3; R.X lands there at L6)
-    } else if (w == 2) {
-        s1 = xget(G, lane);
-        Fe r = fe_sub(s2, s1);
-        r = fe_add(r, r);
-        xput(A, r, lane);
-        xput(B, fe_sqr(r), lane);
-    }
-    __syncthreads();
-    // L5
-    Fe r;
-    if (w == 0) {
-        v = xget(K, lane);
-        r = xget(A, lane);
-        const Fe rr = xget(B, lane);
-        x3 = fe_sub(fe_sub(rr, j), xget(Dd, lane));
-        y3a = fe_mul(r, fe_sub(v, x3));
-    } else if (w == 1) {
-        s1 = xget(G, lane);
-        j = xget(J, lane);
-        const Fe s1j = fe_mul(s1, j);
-        xput(C, fe_add(s1j, s1j), lane);  // 2 s1 j
-    }
-    __syncthreads();
-    // L6
-    if (w == 0) {
-        Jac R;
-        R.X = x3;
-        R.Y = fe_sub(y3a, xget(C, lane));
-        R.Z = xget(I, lane);
-        if (fe_is_zero(acc.Z)) {
-            R = Q;
-        } else if (fe_is_zero(Q.Z)) {
-            R = acc;
-        } else if (fe_is_zero(h)) {
-            R = fe_is_zero(r) ? jac_dbl(acc) : jac_inf();  // acc == Q / acc == -Q (rare: one lane, no barrier)
-        }
-        if (!sel) R = acc;
-        xput(Dd, R.X, lane);
-        xput(E, R.Y, lane);
-        xput(F, R.Z, lane);
-    }
-    __syncthreads();
-    acc.X = xget(Dd, lane);
-    acc.Y = xget(E, lane);
-    acc.Z = xget(F, lane);
-}
-
-#endif  // !FLM_COOP_MODJ
-
-#if FLM_COOP_MODJ
-// ---- modified Jacobian (X, Y, Z, W = Z^4) for the cooperative kernels (FLM_COOP_MODJ, default on)
+// ---- modified Jacobian (X, Y, Z, W = Z^4) for the cooperative kernels 
 // Carrying W takes the doubling's a Z^4 term off the critical path: alpha = 3 (X^2 - W) needs one
 // squaring, so alpha^2 lands one level earlier and a doubling is 3 multiplications of latency and
 // two barriers instead of 4 and three.  Same outputs as dbl-2001-b (X3, Y3, Z3 are identical), so
@@ -1316,18 +1092,15 @@ __device__ __forceinline__ void coop_add_w(JacWT<typename F::E> &acc, bool sel, 
     acc.W = f.get(K, lane);
 }
 
-#endif  // FLM_COOP_MODJ
 
 __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint8_t *__restrict__ points,
                                                                    const uint8_t *__restrict__ scalars,
                                                                    int per_element, int T, int D,
                                                                    uint32_t *__restrict__ jac,
                                                                    uint32_t *__restrict__ flags) {
-#if FLM_COOP_PRIO
     // latency-bound like ec_mul_kernel: beside the unmask on another stream (the unpartitioned
     // overlap, every rank of a sharded reconstruction) these waves issue first
     __builtin_amdgcn_s_setprio(3);
-#endif
     __shared__ __attribute__((aligned(16))) uint32_t S[kCoopSlots * 8 * 64];  // exchange slots, 512 words each
     __shared__ __attribute__((aligned(16))) uint32_t tab[9 * 24 * 64];  // (2t+1) P, t = 0..7, + a spare row
     const int lane = threadIdx.x & 63;
@@ -1349,7 +1122,6 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
         for (int k = 0; k < kNafLen; ++k) dig[k] = 0;
     }
     if (w == 0 && valid && !ok) atomicOr(&flags[i], 2u);
-#if FLM_COOP_MODJ
     // table of odd multiples (2k+1) P (X, Y, Z only: an addend's W is needed on the rare path only)
     JacW PW;
     PW.X = P.X; PW.Y = P.Y; PW.Z = P.Z;
@@ -1406,53 +1178,8 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_coop_kernel(const uint
         if (!ok) acc = jac_inf();
         store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
     }
-#else
-    // table of odd multiples (2k+1) P: 2P into entry 1 as the addend, then entry k = entry k-1 + 2P
-    Jac P2 = P;
-    coop_dbl(P2, w, lane, S);
-    if (w == 0) {
-        xput(tab, P.X, lane);
-        xput(tab + 8 * 64, P.Y, lane);
-        xput(tab + 16 * 64, P.Z, lane);
-        xput(tab + 24 * 64, P2.X, lane);
-        xput(tab + 32 * 64, P2.Y, lane);
-        xput(tab + 40 * 64, P2.Z, lane);
-    }
-    __syncthreads();
-    Jac t = P;
-#pragma unroll 1
-    for (int k = 1; k < 8; ++k) {
-        coop_add(t, true, 1, false, w, lane, S, tab);   // t += 2P (entry 1 holds 2P until the end)
-        if (w == 0) {
-            uint32_t *q = tab + (size_t)(k == 1 ? 8 : k) * 24 * 64;  // (3P lands in a spare row, moved below)
-            xput(q, t.X, lane);
-            xput(q + 8 * 64, t.Y, lane);
-            xput(q + 16 * 64, t.Z, lane);
-        }
-        __syncthreads();
-    }
-    if (w == 0) {  // 3P from the spare row into entry 1
-        const uint32_t *q = tab + (size_t)8 * 24 * 64;
-        xput(tab + 24 * 64, xget(q, lane), lane);
-        xput(tab + 32 * 64, xget(q + 8 * 64, lane), lane);
-        xput(tab + 40 * 64, xget(q + 16 * 64, lane), lane);
-    }
-    __syncthreads();
-    Jac acc = jac_inf();
-#pragma unroll 1
-    for (int k = kNafLen - 1; k >= 0; --k) {
-        coop_dbl(acc, w, lane, S);  // doubling infinity keeps Z = 0: no `started` test needed
-        const int v = dig[k];
-        if (__any(v != 0)) coop_add(acc, v != 0, (v < 0 ? -v : v) >> 1, v < 0, w, lane, S, tab);
-    }
-    if (w == 0 && valid) {
-        if (!ok) acc = jac_inf();
-        store_jac(jac + (size_t)j * 24 * D + i, (size_t)D, acc);
-    }
-#endif
 }
 
-#if FLM_COOP_MODJ
 // The cooperative kernel with every field element spread over a 16-lane row (flm_fe_row.h): a
 // workgroup is the same four waves (formula roles w0..w3 as coop_dbl_w / coop_add_w), each wave
 // holding four scalar multiplications, one per row.  A row multiplication is ~93 instructions per
@@ -1565,137 +1292,14 @@ __global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_kernel(const uint8
     }
 }
 
-// ec_mul_row_kernel with Straus grouping: each 16-lane row sums NT consecutive terms of one pair,
-// sum_u lambda_{jg NT + u} share_{jg NT + u, i}, along ONE chain of doublings (NT tables of odd
-// multiples in LDS, NT digit strings).  Beside the self-mask pass the combine is issue-bound, so
-// what counts is the work per term: (258 / NT + 1) doublings + 50 additions instead of 259 + 50
-// (tools/ec_row_model.py straus_row_model: one G = 8 rank of c5 1.43 -> 1.19 / 1.07 ms predicted at
-// NT = 2 / 4; the chain itself grows to 0.70 / 0.95 ms).  Output: the per-row partial sums as planes
-// [ceil(T / NT)][24][D] for ec_finish_kernel, as ec_mul_straus_kernel.  Terms past T and off-curve
-// points enter as infinity (the latter with flag bit 1).
-template <int NT>
-__global__ __launch_bounds__(64 * kCoopWaves) void ec_mul_row_straus_kernel(const uint8_t *__restrict__ points,
-                                                                         const uint8_t *__restrict__ scalars, int T,
-                                                                         int D, uint32_t *__restrict__ jac,
-                                                                         uint32_t *__restrict__ flags) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ uint32_t S[kCoopSlots * 64];
-    __shared__ uint32_t tab[NT][9 * 3 * 64];
-    const int lane = threadIdx.x & 63, r = lane & 15;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    RowField f;
-    f.K = row::make_ctx();
-    const int Tg = (T + NT - 1) / NT;
-    const size_t g = (size_t)blockIdx.x * 4 + (lane >> 4);
-    const bool valid = g < (size_t)Tg * D;
-    const int jg = valid ? (int)(g / D) : 0;
-    const int i = valid ? (int)(g - (size_t)jg * D) : 0;
-    int8_t dig[NT][kNafLen];
-#pragma unroll 1
-    for (int u = 0; u < NT; ++u) {
-        const int j = jg * NT + u;
-        const bool has = valid && j < T;
-        uint32_t x = 0, y = 0;
-        if (has && r < 8) {
-            const uint32_t *pw = reinterpret_cast<const uint32_t *>(points + ((size_t)j * D + i) * 64);
-            x = __builtin_bswap32(pw[7 - r]);
-            y = __builtin_bswap32(pw[15 - r]);
-        }
-        const uint32_t rhs = f.add(f.sub(f.mul(f.sqr(x), x), f.add(f.add(x, x), x)), r < 8 ? kBn[r & 7] : 0u);
-        const bool in_x = row::row_all8(row::canon(x, f.K) == x, f.K);
-        const bool in_y = row::row_all8(row::canon(y, f.K) == y, f.K);
-        const bool on_c = row::row_all8(row::canon(f.sqr(y), f.K) == row::canon(rhs, f.K), f.K);
-        const bool ok = has && in_x && in_y && on_c;
-        if (w == 0 && has && !ok && r == 0) atomicOr(&flags[i], 2u);
-        JacWT<uint32_t> PW;
-        PW.X = ok ? x : f.one();
-        PW.Y = ok ? y : f.one();
-        PW.Z = ok ? f.one() : 0u;
-        PW.W = PW.Z;
-        if (has) {
-            wnaf5(scalars + (size_t)j * 32, dig[u]);
-        } else {
-#pragma unroll 1
-            for (int k = 0; k < kNafLen; ++k) dig[u][k] = 0;
-        }
-        uint32_t *tu = tab[u];
-        JacWT<uint32_t> P2 = PW;
-        coop_dbl_w(P2, w, lane, S, f);
-        if (w == 0) {
-            tu[0 * 64 + lane] = PW.X;
-            tu[1 * 64 + lane] = PW.Y;
-            tu[2 * 64 + lane] = PW.Z;
-            tu[3 * 64 + lane] = P2.X;
-            tu[4 * 64 + lane] = P2.Y;
-            tu[5 * 64 + lane] = P2.Z;
-        }
-        __syncthreads();
-        JacWT<uint32_t> t = PW;
-#pragma unroll 1
-        for (int k = 1; k < 8; ++k) {
-            coop_add_w(t, true, 1, false, w, lane, S, tu, f);
-            if (w == 0) {
-                uint32_t *q = tu + (size_t)(k == 1 ? 8 : k) * 3 * 64;
-                q[lane] = t.X;
-                q[64 + lane] = t.Y;
-                q[128 + lane] = t.Z;
-            }
-            __syncthreads();
-        }
-        if (w == 0) {
-            const uint32_t *q = tu + (size_t)8 * 3 * 64;
-            tu[3 * 64 + lane] = q[lane];
-            tu[4 * 64 + lane] = q[64 + lane];
-            tu[5 * 64 + lane] = q[128 + lane];
-        }
-        __syncthreads();
-    }
-    JacWT<uint32_t> acc;
-    acc.X = acc.Y = f.one();
-    acc.Z = acc.W = 0u;
-    int vn[NT];
-#pragma unroll
-    for (int u = 0; u < NT; ++u) vn[u] = dig[u][kNafLen - 1];  // one step ahead, as ec_mul_row_kernel
-#pragma unroll 1
-    for (int k = kNafLen - 1; k >= 0; --k) {
-        int v[NT];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            v[u] = vn[u];
-            if (k > 0) vn[u] = dig[u][k - 1];
-        }
-        coop_dbl_w(acc, w, lane, S, f);
-#pragma unroll
-        for (int u = 0; u < NT; ++u)
-            if (__any(v[u] != 0))
-                coop_add_w(acc, v[u] != 0, (v[u] < 0 ? -v[u] : v[u]) >> 1, v[u] < 0, w, lane, S, tab[u], f);
-    }
-    if (w == 0) {
-        const uint32_t rm = r < 8 ? kOne[r & 7] : 0u;
-        const uint32_t X = row::canon(f.mul(acc.X, rm), f.K);
-        const uint32_t Y = row::canon(f.mul(acc.Y, rm), f.K);
-        const uint32_t Z = row::canon(f.mul(acc.Z, rm), f.K);
-        if (valid && r < 8) {
-            uint32_t *o = jac + (size_t)jg * 24 * D + i;
-            o[(size_t)r * D] = X;
-            o[(size_t)(8 + r) * D] = Y;
-            o[(size_t)(16 + r) * D] = Z;
-        }
-    }
-}
-#endif  // FLM_COOP_MODJ
-
 // Per element i: acc = base_i (c1, or infinity when base == nullptr) + sign * sum_j R_{j,i};
 // write the affine wire point and optionally SHA-256(x||y).
 // flags bit 0: base off-curve, bit 1: an input share was off-curve (ec_mul), bit 2: result at infinity.
 // kFinishLanes lanes per element split the T terms (lane q adds j = q, q + kFinishLanes, ...), then
 // log2(kFinishLanes) LDS tree levels add the partials.  At T = 20: 8 lanes make it 3 + 3 sequential
-// additions (lane 0 adds c1 first), 4 lanes 5 + 2 (round 3: 8, FLM_FINISH_LANES for A/B runs).
+// additions (lane 0 adds c1 first), 4 lanes 5 + 2 (round 3: 8).
 // Lane 0 of each element then inverts Z and hashes (the inversion is one lane's chain either way).
-#ifndef FLM_FINISH_LANES
-#define FLM_FINISH_LANES 8
-#endif
-constexpr int kFinishLanes = FLM_FINISH_LANES;
+constexpr int kFinishLanes = 8;
 static_assert(kFinishLanes >= 1 && (kFinishLanes & (kFinishLanes - 1)) == 0 && kFinishLanes <= 64,
               "kFinishLanes: a power of two dividing the workgroup");
 __global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__restrict__ base,
@@ -1739,12 +1343,8 @@ __global__ __launch_bounds__(kEcThreads) void ec_finish_kernel(const uint8_t *__
     if (fe_is_zero(acc.Z)) {
         fl |= 4u;
     } else {
-#if FLM_INV_BINGCD
         // acc.Z is Z R mod p as an integer: (Z R)^-1 R^3 R^-1 = Z^-1 R, the Montgomery form of Z^-1
         Fe zi = fe_mul(fe_inv_bingcd(acc.Z), fe_const(kR3));
-#else
-        Fe zi = fe_inv(acc.Z);
-#endif
         Fe zi2 = fe_sqr(zi);
         x = from_mont(fe_mul(acc.X, zi2));
         y = from_mont(fe_mul(acc.Y, fe_mul(zi2, zi)));
@@ -2115,21 +1715,6 @@ hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int 
                          uint32_t *d_jac, uint32_t *d_flags, hipStream_t stream, int threads, int waves, int coop,
                          int terms, unsigned lds_pad) {
     if (T <= 0 || D <= 0) return hipSuccess;
-#if FLM_COOP_MODJ
-    if (coop == 2 && terms > 1 && !per_element) {  // row field, Straus: terms per row chain
-        const size_t n = (size_t)ec_mul_groups(T, terms) * D;
-        const dim3 grid((unsigned)((n + 3) / 4)), block(64 * kCoopWaves);
-        if (terms == 2)
-            hipLaunchKernelGGL(ec_mul_row_straus_kernel<2>, grid, block, 0, stream, d_points, d_scalars, T, D, d_jac,
-                               d_flags);
-        else if (terms == 4)
-            hipLaunchKernelGGL(ec_mul_row_straus_kernel<4>, grid, block, 0, stream, d_points, d_scalars, T, D, d_jac,
-                               d_flags);
-        else
-            return hipErrorInvalidValue;
-        return hipGetLastError();
-    }
-#endif
     if (terms > 1 && !per_element) {
         const size_t n = (size_t)ec_mul_groups(T, terms) * D;
         const dim3 grid((unsigned)((n + kEcThreads - 1) / kEcThreads));
@@ -2143,14 +1728,12 @@ hipError_t launch_ec_mul(const uint8_t *d_points, const uint8_t *d_scalars, int 
             return hipErrorInvalidValue;
         return hipGetLastError();
     }
-#if FLM_COOP_MODJ
     if (coop == 2) {  // one element per 16-lane row: four scalar multiplications per workgroup
         const size_t n = (size_t)T * D;
         hipLaunchKernelGGL(ec_mul_row_kernel, dim3((unsigned)((n + 3) / 4)), dim3(64 * kCoopWaves), 0, stream,
                            d_points, d_scalars, per_element, T, D, d_jac, d_flags);
         return hipGetLastError();
     }
-#endif
     if (coop) {
         const size_t n = (size_t)T * D;
         hipLaunchKernelGGL(ec_mul_coop_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kCoopWaves), 0, stream,

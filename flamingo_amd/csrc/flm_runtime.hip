@@ -103,6 +103,25 @@ struct StageSlot {
 
 using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>;
 
+// A device seed table: the per-seed schedule seed_schedule_kernel builds (SeedRec per seed) and
+// its sign counts (meta), read by items_kernel / pair_units_kernel.  A context keeps a ring of
+// them so that a call on one stream never rewrites a table that launches queued on other streams
+// still read (the r05 cross-stream hazard): each table records its write
+// (`written`, on `w_stream`) and its last read on every stream (`readers`).  A table is rebuilt on
+// stream s only once every read and write of it on other streams has completed; when all
+// kSeedTables tables are still in use elsewhere, s waits on the device for the least recently used
+// one's events (hipStreamWaitEvent, never a host wait).  Reads on the writing stream are in order
+// by construction; a read on another stream (a published table used by flm_aggregate_dev there)
+// waits for `written` first.
+constexpr size_t kSeedTables = 8;
+struct SeedTable {
+    DevBuf recs, meta;
+    hipEvent_t written = nullptr;
+    hipStream_t w_stream = nullptr;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
+    uint64_t last_use = 0;
+};
+
 }  // namespace
 
 // flm_last_plan's variant for a round run by small_round_kernel (items = its workgroups)
@@ -112,7 +131,11 @@ struct flm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    DevBuf rows, out, seeds, signs, recs, meta, bytes_in, bytes_out;
+    DevBuf rows, out, seeds, signs, bytes_in, bytes_out;
+    std::vector<SeedTable *> tables;  // ring of device seed tables (SeedTable)
+    SeedTable *cur_table = nullptr;   // the table the last seed-schedule / small-round launch wrote
+    SeedTable *pub_table = nullptr;   // the table flm_seed_table_dev published for flm_aggregate_dev
+    uint64_t table_clock = 0;
     std::vector<StageSlot *> slots;  // staging pool of the *_dev uploads (StageSlot)
     uint64_t slot_clock = 0;
     DevBuf ec_in, ec_base, ec_scal, ec_jac, ec_out, ec_dig, ec_flags;  // P-256 batches
@@ -128,7 +151,7 @@ struct flm_ctx {
     std::map<PlanKey, Plan *> plans;
     uint64_t plan_clock = 0;
     int last_items = 0, last_tile = 0, last_atomics = 0, last_variant = 0;
-    int table_k = -1;  // seeds in the current device seed table
+    int table_k = -1;  // seeds in the published device seed table (pub_table), -1 = none
     int tune_variant = -1;   // items_kernel variant, -1 = auto
     int tune_subtiles = 0;   // aggregate sub-tiles per workgroup, 0 = auto
     int tune_min_items = 1024;  // planner target for work items per aggregate launch (kDefaultMinItems)
@@ -137,7 +160,6 @@ struct flm_ctx {
     int tune_ec_spread = 0;     // KiB of LDS reserved per 64-lane EC workgroup (0 = none): caps EC waves per CU
                                 // so a CU-masked dispatch spreads them one per SIMD instead of packing two
     int tune_ec_terms = 1;      // combine terms per lane (1, 2, 4: Straus, shared doublings)
-    int tune_ec_row_terms = 1;  // combine terms per row chain of the row-field kernel (1, 2, 4: Straus)
     int tune_ec_coop = -1;      // 1: four waves per 64 scalar multiplications (ec_mul_coop_kernel); 2: four
                                 // waves per 4, each element on a 16-lane row (ec_mul_row_kernel); 0: one
                                 // lane each; -1 (auto): cooperative when the batch fits one pass of the chip
@@ -439,9 +461,6 @@ void plan_free(Plan *plan) {
 }
 
 constexpr size_t kPlanCache = 64;        // launch plans kept per context (shapes)
-#ifndef FLM_PLAN_DONE_EVENTS
-#define FLM_PLAN_DONE_EVENTS 1  // 0: A/B builds only (recycling then has no completion to wait for)
-#endif
 constexpr int kDefaultMinItems = 1024;   // flm_set_tuning("min_items") default
 constexpr uint64_t kUnsplitTiles = 1024;  // 4 tiles per MI355X CU: from this many a whole-vector round is not split
 constexpr uint64_t kSplitItems = 2048;    // item target of a split whole-vector round (8 per CU)
@@ -650,32 +669,153 @@ int small_round_width(const flm_ctx *ctx, int N, int K, uint64_t L, uint64_t mas
     return L >= (1ull << 16) ? 4 : 2;
 }
 
+// True when the event has completed (or was never recorded); false while it is pending.
+bool event_done(hipEvent_t e) {
+    if (!e) return true;
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    (void)hipGetLastError();  // hipErrorNotReady (an error status would surface at the next launch)
+    return false;
+}
+
+// No read or write of `t` on a stream other than s is still pending: s may rewrite it at once.
+bool table_free_on(const SeedTable *t, hipStream_t s) {
+    if (t->w_stream != s && !event_done(t->written)) return false;
+    for (const auto &r : t->readers)
+        if (r.first != s && !event_done(r.second)) return false;
+    return true;
+}
+
+// A seed table stream s may overwrite, grown to hold K records and `meta_words` sign-count words
+// (SeedTable).  The write launch follows on s; table_written() records it.
+SeedTable *table_acquire(flm_ctx *ctx, int K, size_t meta_words, hipStream_t s, int *rc) {
+    SeedTable *t = nullptr;
+    for (SeedTable *c : ctx->tables)  // the least recently used of the tables s may rewrite at once
+        if (table_free_on(c, s) && (!t || c->last_use < t->last_use)) t = c;
+    if (!t && ctx->tables.size() < kSeedTables) {
+        t = new SeedTable();
+        if (hipEventCreateWithFlags(&t->written, hipEventDisableTiming) != hipSuccess) {
+            delete t;
+            *rc = fail(ctx, FLM_EHIP, "seed table: hipEventCreate failed");
+            return nullptr;
+        }
+        ctx->tables.push_back(t);
+    }
+    if (!t) {  // every table is still in use on other streams: s waits (on the device) for the oldest
+        t = ctx->tables.front();
+        for (SeedTable *c : ctx->tables)
+            if (c->last_use < t->last_use) t = c;
+        hipError_t e = hipSuccess;
+        if (t->w_stream != s) e = hipStreamWaitEvent(s, t->written, 0);
+        for (const auto &r : t->readers)
+            if (e == hipSuccess && r.first != s) e = hipStreamWaitEvent(s, r.second, 0);
+        if (e != hipSuccess) {
+            *rc = fail(ctx, FLM_EHIP, "seed table: hipStreamWaitEvent failed: %s", hipGetErrorString(e));
+            return nullptr;
+        }
+    }
+    // growing frees the old buffer: hipFree waits for the device, so no pending launch reads it
+    hipError_t e = t->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec));
+    if (e == hipSuccess) e = t->meta.reserve(sizeof(uint32_t) * std::max<size_t>(4, meta_words));
+    if (e != hipSuccess) {
+        *rc = fail(ctx, FLM_ENOMEM, "seed table of %d seeds: %s", K, hipGetErrorString(e));
+        return nullptr;
+    }
+    t->last_use = ++ctx->table_clock;
+    if (ctx->pub_table == t) {  // never left published while it holds other seeds
+        ctx->pub_table = nullptr;
+        ctx->table_k = -1;
+    }
+    *rc = 0;
+    return t;
+}
+
+// The table's write launch has been enqueued on s.
+hipError_t table_written(flm_ctx *ctx, SeedTable *t, hipStream_t s) {
+    t->w_stream = s;
+    ctx->cur_table = t;
+    return hipEventRecord(t->written, s);
+}
+
+// Before a launch on s that reads t: order it after t's write when that ran on another stream.
+hipError_t table_before_read(SeedTable *t, hipStream_t s) {
+    if (t->w_stream == s || event_done(t->written)) return hipSuccess;
+    return hipStreamWaitEvent(s, t->written, 0);
+}
+
+// A launch that reads t has been enqueued on s: record it as the table's last read on s (one event
+// per stream, reused; entries of finished streams are pruned as in Plan::done).
+hipError_t table_read(SeedTable *t, hipStream_t s) {
+    hipEvent_t *ev = nullptr;
+    for (auto &r : t->readers)
+        if (r.first == s) ev = &r.second;
+    if (!ev) {
+        if (t->readers.size() >= 8) {
+            std::vector<std::pair<hipStream_t, hipEvent_t>> keep;
+            for (auto &r : t->readers) {
+                if (event_done(r.second)) (void)hipEventDestroy(r.second);
+                else keep.push_back(r);
+            }
+            t->readers.swap(keep);
+        }
+        hipEvent_t e = nullptr;
+        const hipError_t c = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (c != hipSuccess) return c;
+        t->readers.emplace_back(s, e);
+        ev = &t->readers.back().second;
+    }
+    return hipEventRecord(*ev, s);
+}
+
+void table_free(SeedTable *t) {
+    if (t->written) (void)hipEventSynchronize(t->written);
+    for (auto &r : t->readers) (void)hipEventSynchronize(r.second);
+    t->recs.release();
+    t->meta.release();
+    if (t->written) (void)hipEventDestroy(t->written);
+    for (auto &r : t->readers) (void)hipEventDestroy(r.second);
+    delete t;
+}
+
+// The one-launch small round writes its sign counts into a seed table's meta (flm_check_signs)
+// and builds no records, so it unpublishes the table like every other rebuild.
 int run_small_round(flm_ctx *ctx, int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
                     const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi, uint64_t prg_slot0,
-                    uint32_t *d_out, DevBuf &meta, hipStream_t s) {
-    FLM_HIP(ctx, meta.reserve(4 * sizeof(uint32_t)));
+                    uint32_t *d_out, hipStream_t s) {
+    int rc = 0;
+    SeedTable *t = table_acquire(ctx, 0, 4, s, &rc);
+    if (!t) return rc;
     FLM_HIP(ctx, flm::launch_small_round(B, d_rows, pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi,
-                                         (uint32_t)(prg_slot0 / 16), d_out, meta.as<uint32_t>(), s));
+                                         (uint32_t)(prg_slot0 / 16), d_out, t->meta.as<uint32_t>(), s));
+    FLM_HIP(ctx, table_written(ctx, t, s));
+    ctx->pub_table = nullptr;
+    ctx->table_k = -1;
     return 0;
 }
 
-// zero_out (optional): the round's output, zero-filled by the same launch (zero_n words).
-// Only flm_seed_table_dev publishes the table for a later flm_aggregate_dev (publish = true); every
-// other entry point that rebuilds it (prg expansion, client masking, pair units, the fused round)
-// invalidates it, so aggregate_dev can never unmask against seeds it was not given.
+// Build a seed table on s (returned in *out).  zero_out (optional): the round's output,
+// zero-filled by the same launch (zero_n words).  Only flm_seed_table_dev publishes the table for a
+// later flm_aggregate_dev (publish = true); every other entry point that builds one (prg expansion,
+// client masking, pair units, the fused round) withdraws the publication, so aggregate_dev only
+// ever unmasks against the seeds of the latest flm_seed_table_dev call, and only until another
+// entry point runs.
 int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, hipStream_t s,
-                      uint32_t *zero_out = nullptr, uint64_t zero_n = 0, bool publish = false) {
-    FLM_HIP(ctx, ctx->recs.reserve(std::max<size_t>(1, (size_t)K) * sizeof(SeedRec)));
+                      SeedTable **out, uint32_t *zero_out = nullptr, uint64_t zero_n = 0, bool publish = false) {
     const int groups = flm::seed_schedule_groups(K, zero_out ? zero_n : 0);
-    FLM_HIP(ctx, ctx->meta.reserve(sizeof(uint32_t) * (2 + 2 * (size_t)groups)));
-    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), s,
+    int rc = 0;
+    SeedTable *t = table_acquire(ctx, K, 2 + 2 * (size_t)groups, s, &rc);
+    if (!t) return rc;
+    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, t->recs.as<SeedRec>(), t->meta.as<uint32_t>(), s,
                                            zero_out, zero_n));
+    FLM_HIP(ctx, table_written(ctx, t, s));
+    ctx->pub_table = publish ? t : nullptr;
     ctx->table_k = publish ? K : -1;
+    *out = t;
     return 0;
 }
 
 // zeroed: the output was already zero-filled on this stream (by the seed-schedule launch)
-int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
+int run_plan(flm_ctx *ctx, Plan &plan, SeedTable *table, const uint32_t *d_rows, uint64_t pitch, uint32_t *d_out,
              size_t out_elems, hipStream_t s, bool zeroed = false) {
     if (!plan.ready_known) {  // the items' copy was enqueued on another stream: order after it
         const hipError_t q = hipEventQuery(plan.ready);
@@ -685,9 +825,10 @@ int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, u
     }
     if (plan.needs_zero && !zeroed) FLM_HIP(ctx, hipMemsetAsync(d_out, 0, out_elems * sizeof(uint32_t), s));
     const int variant_id = pick_variant(ctx, plan);
+    FLM_HIP(ctx, table_before_read(table, s));
     FLM_HIP(ctx, flm::launch_items(plan.subtiles, variant_id, plan.items.as<Item>(), plan.n_items, d_rows, pitch,
-                                   ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s));
-#if FLM_PLAN_DONE_EVENTS
+                                   table->recs.as<SeedRec>(), table->meta.as<uint32_t>(), d_out, s));
+    FLM_HIP(ctx, table_read(table, s));
     // one event per stream the plan ran on, after its last launch there: the cache recycles the
     // items only once all of them have completed (no dependency is added between the streams)
     hipEvent_t *ev = nullptr;
@@ -709,7 +850,6 @@ int run_plan(flm_ctx *ctx, Plan &plan, const uint32_t *d_rows, uint64_t pitch, u
         ev = &plan.done.back().second;
     }
     FLM_HIP(ctx, hipEventRecord(*ev, s));
-#endif
     ctx->last_items = plan.n_items;
     ctx->last_tile = flm::kWaveSlots * plan.subtiles;
     ctx->last_atomics = plan.atomics;
@@ -895,15 +1035,17 @@ int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, cons
     }
     FLM_HIP(ctx, stage_upload(slot, item_bytes + (size_t)K, s));
     const uint8_t *d = slot->dev.as<uint8_t>();
-    rc = run_seed_schedule(ctx, d_seeds, reinterpret_cast<const int8_t *>(d + item_bytes), K, s);
+    SeedTable *table = nullptr;
+    rc = run_seed_schedule(ctx, d_seeds, reinterpret_cast<const int8_t *>(d + item_bytes), K, s, &table);
     if (!rc && needs_zero) {
         const hipError_t e = hipMemsetAsync(d_out, 0, (size_t)N * pitch * sizeof(uint32_t), s);
         if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
     }
     const int variant_id = pick_variant(ctx, plan);
     if (!rc && plan.n_items) {
-        const hipError_t e = flm::launch_items(subtiles, variant_id, reinterpret_cast<const Item *>(d), plan.n_items,
-                                               d_x, pitch, ctx->recs.as<SeedRec>(), ctx->meta.as<uint32_t>(), d_out, s);
+        hipError_t e = flm::launch_items(subtiles, variant_id, reinterpret_cast<const Item *>(d), plan.n_items, d_x,
+                                         pitch, table->recs.as<SeedRec>(), table->meta.as<uint32_t>(), d_out, s);
+        if (e == hipSuccess) e = table_read(table, s);
         if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "items launch: %s", hipGetErrorString(e));
     }
     // the slot is busy until the work enqueued so far has run, whether or not it all got enqueued
@@ -950,7 +1092,7 @@ int flm_device_count(void) {
     return n;
 }
 
-const char *flm_version(void) { return "flamingo_hip 0.3 gfx950 items_kernel<S={1,4,16}>"; }
+const char *flm_version(void) { return "flamingo_hip 0.4 gfx950 items_kernel<S={1,4,16}>"; }
 
 int flm_init(flm_ctx **out, int device) {
     if (!out) return fail(nullptr, FLM_EINVAL, "flm_init: out is NULL");
@@ -979,12 +1121,15 @@ void flm_free(flm_ctx *ctx) {
     if (!ctx) return;
     flm::rt::DeviceScope dev_scope_(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // collectives may sit on a caller's stream (a torch comm stream), not the context's: the whole
+    // device completes before the communicator is finalised (flm_comm_destroy does the same)
+    if (ctx->comm) (void)hipDeviceSynchronize();
     flm::comm_release(ctx);
     for (StageSlot *s : ctx->slots) (void)hipEventSynchronize(s->done);  // launches on other streams
     for (auto &kv : ctx->plans) plan_free(kv.second);
-    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->recs, &ctx->meta, &ctx->bytes_in,
-                      &ctx->bytes_out, &ctx->ec_in, &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out,
-                      &ctx->ec_dig, &ctx->ec_flags})
+    for (SeedTable *t : ctx->tables) table_free(t);  // waits for the table's readers on every stream
+    for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->bytes_in, &ctx->bytes_out, &ctx->ec_in,
+                      &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out, &ctx->ec_dig, &ctx->ec_flags})
         b->release();
     for (StageSlot *s : ctx->slots) {
         if (s->host) (void)hipHostFree(s->host);
@@ -1057,7 +1202,8 @@ int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     if (K > 0 && (!d_seeds || !d_signs)) return fail(ctx, FLM_EINVAL, "seeds/signs NULL");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_ON_DEVICE(ctx);
-    return run_seed_schedule(ctx, d_seeds, d_signs, K, s, nullptr, 0, /*publish=*/true);
+    SeedTable *t = nullptr;
+    return run_seed_schedule(ctx, d_seeds, d_signs, K, s, &t, nullptr, 0, /*publish=*/true);
 }
 
 int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,
@@ -1065,13 +1211,14 @@ int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, in
     if (!ctx) return fail(nullptr, FLM_EINVAL, "ctx is NULL");
     if (L == 0) return 0;
     if (int rc = check_aggregate_args(ctx, d_rows, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, d_out)) return rc;
-    if (K != ctx->table_k) return fail(ctx, FLM_EINVAL, "K=%d does not match the seed table (%d)", K, ctx->table_k);
+    if (!ctx->pub_table || K != ctx->table_k)
+        return fail(ctx, FLM_EINVAL, "K=%d does not match the seed table (%d)", K, ctx->table_k);
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_ON_DEVICE(ctx);
     int rc = 0;
     Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, s, &rc);
     if (!plan) return rc;
-    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s);
+    return run_plan(ctx, *plan, ctx->pub_table, d_rows, row_pitch, d_out, L, s);
 }
 
 int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, const uint8_t *d_seeds,
@@ -1087,9 +1234,8 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     if (const int B = small_round_width(ctx, N, K, L, mask_lo, mask_hi)) {
         // one submission; the device seed table is not built, so flm_aggregate_dev must not reuse it
         if ((rc = run_small_round(ctx, B, d_rows, row_pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi, prg_slot0,
-                                  d_out, ctx->meta, s)))
+                                  d_out, s)))
             return rc;
-        ctx->table_k = -1;
         ctx->last_items = (int)((L + flm::small_round_slots(B) - 1) / flm::small_round_slots(B));
         ctx->last_tile = flm::small_round_slots(B);
         ctx->last_atomics = 0;
@@ -1099,8 +1245,9 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     Plan *plan = aggregate_plan(ctx, row_pitch, N, K, L, mask_lo, mask_hi, prg_slot0, s, &rc);
     if (!plan) return rc;
     // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
-    if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, plan->needs_zero ? d_out : nullptr, L))) return rc;
-    return run_plan(ctx, *plan, d_rows, row_pitch, d_out, L, s, plan->needs_zero);
+    SeedTable *table = nullptr;
+    if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, &table, plan->needs_zero ? d_out : nullptr, L))) return rc;
+    return run_plan(ctx, *plan, table, d_rows, row_pitch, d_out, L, s, plan->needs_zero);
 }
 
 int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,
@@ -1308,9 +1455,6 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "ec_terms") {
         if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_terms must be 1, 2 or 4");
         ctx->tune_ec_terms = value;
-    } else if (k == "ec_row_terms") {
-        if (value != 1 && value != 2 && value != 4) return fail(ctx, FLM_EINVAL, "ec_row_terms must be 1, 2 or 4");
-        ctx->tune_ec_row_terms = value;
     } else if (k == "ec_coop") {
         if (value < -1 || value > 2) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0, 1 or 2");
         ctx->tune_ec_coop = value;
@@ -1324,14 +1468,36 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     return 0;
 }
 
+int flm_get_tuning(const flm_ctx *ctx, const char *key, int *value) {
+    flm_ctx *c = const_cast<flm_ctx *>(ctx);  // only its error string is written
+    if (!ctx || !key || !value) return fail(c, FLM_EINVAL, "NULL argument");
+    const std::string k(key);
+    const std::pair<const char *, int> knobs[] = {
+        {"variant", ctx->tune_variant},       {"pairing", ctx->tune_pairing},     {"subtiles", ctx->tune_subtiles},
+        {"ec_waves", ctx->tune_ec_waves},     {"small", ctx->tune_small},         {"min_items", ctx->tune_min_items},
+        {"ec_spread", ctx->tune_ec_spread},   {"ec_terms", ctx->tune_ec_terms},   {"ec_coop", ctx->tune_ec_coop},
+        {"ec_threads", ctx->tune_ec_threads}};
+    for (const auto &kv : knobs)
+        if (k == kv.first) {
+            *value = kv.second;
+            return 0;
+        }
+    return fail(c, FLM_EINVAL, "unknown tuning key '%s'", key);
+}
+
 int flm_check_signs(flm_ctx *ctx, int *bad_count) {
     if (!ctx || !bad_count) return fail(ctx, FLM_EINVAL, "NULL argument");
     *bad_count = 0;
-    if (!ctx->meta.p) return 0;
+    const SeedTable *t = ctx->cur_table;
+    if (!t) return 0;
+    FLM_ON_DEVICE(ctx);
+    FLM_HIP(ctx, hipEventSynchronize(t->written));
     uint32_t parts = 0;
-    FLM_HIP(ctx, hipMemcpy(&parts, ctx->meta.p, sizeof parts, hipMemcpyDeviceToHost));
+    FLM_HIP(ctx, hipMemcpy(&parts, t->meta.p, sizeof parts, hipMemcpyDeviceToHost));
+    if (2 + 2 * (size_t)parts > t->meta.cap / sizeof(uint32_t))
+        return fail(ctx, FLM_EHIP, "seed table sign counts: %u parts overrun the table", parts);
     std::vector<uint32_t> m(2 + 2 * (size_t)parts);
-    FLM_HIP(ctx, hipMemcpy(m.data(), ctx->meta.p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    FLM_HIP(ctx, hipMemcpy(m.data(), t->meta.p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (uint32_t p = 0; p < parts; ++p) *bad_count += (int)m[3 + 2 * p];
     return 0;
 }
@@ -1380,7 +1546,7 @@ int flm_ec_combine_dev(flm_ctx *ctx, const uint8_t *d_c1, const uint8_t *d_share
     FLM_HIP(ctx, ctx->ec_jac.reserve((size_t)std::max(T, 1) * D * 96));
     FLM_HIP(ctx, hipMemsetAsync(d_flags, 0, (size_t)D * 4, s));
     const int coop = ec_coop(ctx, (size_t)T * D);
-    const int terms = coop == 2 ? ctx->tune_ec_row_terms : (coop ? 1 : ctx->tune_ec_terms);
+    const int terms = coop ? 1 : ctx->tune_ec_terms;
     FLM_HIP(ctx, flm::launch_ec_mul(d_shares, d_lambdas, 0, T, D, ctx->ec_jac.as<uint32_t>(), d_flags, s,
                                     ctx->tune_ec_threads, ctx->tune_ec_waves, coop, terms,
                                     1024u * (unsigned)ctx->tune_ec_spread));
@@ -1455,8 +1621,10 @@ int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (final_pass) FLM_HIP(ctx, flm::launch_add2(d_p0, d_p1, d_dst, L, s));
     if (L == 0 || K == 0) return 0;
-    if (int rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s)) return rc;
-    FLM_HIP(ctx, flm::launch_pair_units(!final_pass, ctx->recs.as<flm::SeedRec>(), K, d_dst, L, d_ws, groups, s));
+    SeedTable *table = nullptr;
+    if (int rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, &table)) return rc;
+    FLM_HIP(ctx, flm::launch_pair_units(!final_pass, table->recs.as<flm::SeedRec>(), K, d_dst, L, d_ws, groups, s));
+    FLM_HIP(ctx, table_read(table, s));
     return 0;
 }
 

@@ -117,20 +117,16 @@ class MaskEngine:
         if rc != 0:
             raise RuntimeError(f"{what}: {self.lib.flm_last_error(self.ctx).decode()} (code {rc})")
 
-    # flm_set_tuning defaults (include/flamingo_hip.h), for get_tuning before any set_tuning
-    TUNING_DEFAULTS = {"variant": -1, "subtiles": 0, "pairing": 1, "min_items": 1024, "ec_threads": 64,
-                       "ec_waves": 1, "ec_coop": -1, "ec_terms": 1, "ec_row_terms": 1, "ec_spread": 0,
-                       "small": 1}
-
     def set_tuning(self, key: str, value: int):
-        """A/B knobs: variant (-1 auto, 0..3) and subtiles (0 auto, 1, 4, 16)."""
+        """A/B knobs (flm_set_tuning, include/flamingo_hip.h): variant, subtiles, pairing, ..."""
         self._check(self.lib.flm_set_tuning(self.ctx, key.encode(), int(value)), f"flm_set_tuning({key})")
-        self.__dict__.setdefault("_tuning", {})[key] = int(value)
 
     def get_tuning(self, key: str) -> int:
-        """The value set_tuning last gave `key` on this engine (else the library default)."""
-        t = self.__dict__.get("_tuning", {})
-        return t[key] if key in t else self.TUNING_DEFAULTS[key]
+        """The context's current value of `key` (flm_get_tuning): also what another wrapper of the
+        same flm_ctx (DeviceGroup engines, a direct flm_set_tuning call) set."""
+        v = ctypes.c_int()
+        self._check(self.lib.flm_get_tuning(self.ctx, key.encode(), ctypes.byref(v)), f"flm_get_tuning({key})")
+        return v.value
 
     def last_plan(self) -> dict:
         v = [ctypes.c_int() for _ in range(4)]

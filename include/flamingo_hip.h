@@ -26,9 +26,12 @@
  *    (a hipStream_t; NULL = the HIP null stream) and return without waiting
  *    for earlier work: the small tables they upload (seg/signs, work items)
  *    go through a pool of pinned staging slots, each reused only after the
- *    launch that read it has completed.  A context's device seed table is
- *    shared by its calls: calls of one context on different streams either
- *    use the same seeds or are ordered by the caller (or use a context each).
+ *    launch that read it has completed.  The per-seed device tables a call
+ *    builds come from a ring (8 per context) with the same rule: a table is
+ *    rebuilt on a stream only after every launch on other streams that reads
+ *    it has completed (or, when all are in use, that stream waits for them on
+ *    the device), so calls of one context may run on any mix of streams with
+ *    any seeds, without ordering by the caller.
  *  - One context per host thread; a context binds one GPU (one process per
  *    GPU).  Create it lazily, after any fork (SA_ServiceAgent.py:562 forks a
  *    multiprocessing.Pool).
@@ -122,8 +125,12 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
  * dominant kernel alone: flm_seed_table_dev builds the context's per-seed
  * schedule (ChaCha key words, sign, counter-independent first-round words)
  * from device seeds/signs; flm_aggregate_dev then runs the row-sum + unmask
- * kernel against that table (K must match the table).  Same requirements as
- * flm_aggregate_unmask_dev. */
+ * kernel against that table (K must match the table), on any stream: a read
+ * on another stream than the table's build waits for the build on the device.
+ * The table stays published until the context's next call that builds a seed
+ * table (any *_dev round, expansion, client masking, pair units, or another
+ * flm_seed_table_dev); flm_aggregate_dev then fails with FLM_EINVAL rather
+ * than unmask against other seeds.  Same requirements as flm_aggregate_unmask_dev. */
 int flm_seed_table_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_signs, int K, void *stream);
 int flm_aggregate_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L,
                       size_t mask_lo, size_t mask_hi, uint64_t prg_slot0, uint32_t *d_out, void *stream);
@@ -176,9 +183,6 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *   "ec_terms" 1 (default) | 2 | 4: products summed per lane in the reconstruction combine
  *              (Straus: the terms share one chain of doublings); ignored when the combine
  *              runs cooperatively.
- *   "ec_row_terms" 1 (default) | 2 | 4: the same Straus grouping inside the row-field cooperative
- *              kernel (ec_coop 2): each 16-lane row sums that many terms of one pair along one
- *              chain of doublings (less issue work per term, a longer chain).
  *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
  *              per-lane combine kernels (caps their workgroups per CU).
  *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev runs
@@ -187,6 +191,8 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              mask_hi == L).  That path builds no device seed table: a following
  *              flm_aggregate_dev needs its own flm_seed_table_dev. */
 int flm_set_tuning(flm_ctx *ctx, const char *key, int value);
+/* The context's current value of a flm_set_tuning key (whoever set it), FLM_EINVAL for an unknown key. */
+int flm_get_tuning(const flm_ctx *ctx, const char *key, int *value);
 
 /* Host-only view of the launch planner (no GPU needed): the work items the
  * aggregate kernel would run for this round shape.  items_out receives up to

@@ -63,10 +63,14 @@ def main():
            "dst": ecchash_dst(),
            "count": ALL,
            "table_sha256": hashlib.sha256(b"".join(rows)).hexdigest(),
+           "parity": PARITY_NOTE,
            "points": {str(v): rows[v].hex() for v in sample}}
     with open(os.path.join(HERE, "h2c_golden.json"), "w") as f:
         json.dump(rec, f, indent=0, sort_keys=True)
     print("table_sha256", rec["table_sha256"], len(rec["points"]), "sample points")
+
+
+PARITY_NOTE = ("parity unpinned: libnum's sqrtmod root order (ecchash.py:263-268) -- the table assumes the root a^((p+1)/4) is yielded first; libnum is absent here and no reference-held fixture pins it")
 
 
 def ecchash_dst():

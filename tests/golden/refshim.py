@@ -30,11 +30,13 @@ What each stand-in is, and how faithful:
   polynomials are reproducible and recorded.
 * ``libnum.invmod / has_sqrtmod / sqrtmod`` -- modular inverse, Euler's
   criterion, and for p = 3 (mod 4) the roots a^((p+1)/4) then p - a^((p+1)/4).
-  ASSUMPTION (the one convention not pinned): that libnum 1.7's
-  sqrtmod_prime_power yields the direct root first.  It only affects which of
+  ASSUMPTION (the one convention not pinned -- parity unpinned): that libnum
+  1.7's sqrtmod_prime_power yields the direct root first.  It decides which of
   the two hash-to-curve points (x, +-y) a pair seed s_ij is hashed from
-  (ecchash.py:263-268); the mask arithmetic downstream of s_ij does not depend
-  on it.
+  (ecchash.py:263-268; sgn0 at :227-231,271-272 flips y only when u or y is 0),
+  so s_ij = SHA-256(x||y) and every pairwise PRG mask depend on it.  Only the
+  cancellation of the masks within one simulation (every party uses the same
+  convention) is independent of it.
 """
 from __future__ import annotations
 

@@ -103,3 +103,21 @@ def test_pmc_child_env_leaves_the_ranks_group():
                            "MASTER_PORT": "29500", "TORCHELASTIC_RUN_ID": "x", "PATH": "/usr/bin",
                            "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     assert env == {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0", "TMPDIR": "/tmp"}
+
+
+def test_scaling_check_fields():
+    """A G > 1 line carries the self-check a first 8-GPU run is read with:
+    the RCCL communicator's rank count, the one-GPU model's per-rank kernel time and value for
+    that G, and measured / predicted."""
+    b = 4.0 * 1024 * (1 << 20) + 4.0 * (1 << 20)
+    r = bench.scaling_check(8, True, 1024, 1 << 20, [0.19, 0.2], 20000.0, b, 8, "rccl")
+    assert r["rccl_ranks_ok"] is True and r["rccl_comm_ranks"] == 8
+    assert r["predicted_rank_kernel_ms"] == 0.184 and r["measured_rank_kernel_ms_max"] == 0.2
+    assert abs(r["predicted_value_gbs"] - b / 0.184e-3 / 1e9) < 0.1
+    assert abs(r["predicted_vs_measured"]["rank_kernel_ms"] - 0.2 / 0.184) < 1e-3
+    assert abs(r["predicted_vs_measured"]["value"] - 20000.0 / r["predicted_value_gbs"]) < 1e-3
+    # gloo (no library communicator) or another shape: the fields are there, the model is not applied
+    g = bench.scaling_check(2, True, 64, 1 << 16, [1.0, 1.1], 10.0, 1.0, None, "torch")
+    assert g["rccl_ranks_ok"] is False and g["predicted_rank_kernel_ms"] is None
+    assert g["predicted_vs_measured"] is None
+    assert set(g) == set(r)

@@ -53,3 +53,6 @@ def test_bench_spawns_its_own_ranks():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["correct"] is True
     assert res["comm"]["world"] == 2 and res["comm"]["backend"] == "gloo"
+    sc = res["scaling_check"]                     # the self-check fields of a G > 1 line (bench.scaling_check)
+    assert sc["rccl_ranks_ok"] is False and sc["rccl_comm_ranks"] is None   # gloo: no library communicator
+    assert len(res["roofline"]["kernel_ms_per_rank"]["ranks"]) == 2 and "predicted_vs_measured" in sc

@@ -17,19 +17,17 @@ import ec_oracle as E
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[(0, 1, 1), (1, 1, 1), (2, 1, 1), (0, 2, 1), (0, 4, 1), (2, 1, 2), (2, 1, 4)],
-                ids=["per_lane", "coop", "row", "straus2", "straus4", "row_straus2", "row_straus4"])
+@pytest.fixture(scope="module", params=[(0, 1), (1, 1), (2, 1), (0, 2), (0, 4)],
+                ids=["per_lane", "coop", "row", "straus2", "straus4"])
 def eng(request):
     """Every test runs with each scalar-multiplication kernel: one lane per product (ec_mul_kernel),
     four cooperating waves per 64 products (ec_mul_coop_kernel), the same with every field element
-    on a 16-lane row (ec_mul_row_kernel, flm_fe_row.h), 2 / 4 combine terms per lane sharing one
-    chain of doublings (ec_mul_straus_kernel), and 2 / 4 terms per row chain of the row kernel
-    (ec_mul_row_straus_kernel; the combine only, T = 3 leaves a partial group)."""
+    on a 16-lane row (ec_mul_row_kernel, flm_fe_row.h), and 2 / 4 combine terms per lane sharing
+    one chain of doublings (ec_mul_straus_kernel; the combine only, T = 3 leaves a partial group)."""
     from flamingo_amd import MaskEngine
     e = MaskEngine(0)
     e.set_tuning("ec_coop", request.param[0])
     e.set_tuning("ec_terms", request.param[1])
-    e.set_tuning("ec_row_terms", request.param[2])
     yield e
     e.close()
 

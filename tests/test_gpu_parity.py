@@ -156,7 +156,7 @@ def test_plan_cache_recycles_past_its_capacity():
 
 def test_plan_cache_recycling_across_streams():
     """One shape launched on two streams behind long queued work, then more new shapes (mask
-    windows of the same seeds, so the context's shared seed table stays valid, include/flamingo_hip.h)
+    windows of the same seeds; test_seed_table_across_streams_varying_k varies the seeds too)
     than the cache holds, on a third stream, while those launches may still run: the recycled plan's
     item buffer is reused only after every launch of it (its `done` event, the second stream's
     launch ordered after the first's)."""
@@ -190,6 +190,119 @@ def test_plan_cache_recycling_across_streams():
         got = last.cpu().numpy().view(np.uint32)
         assert np.array_equal(got[:hi], want[:hi])
         assert np.array_equal(got[hi:], rows[:, hi:].sum(axis=0, dtype=np.uint64).astype(np.uint32))
+
+
+def _queue_matmuls(n=20):
+    """Queue ~tens of ms of work on the current stream, so what follows it there stays pending."""
+    import torch
+    a = torch.randn(2048, 2048, device="cuda")
+    for _ in range(n):
+        a = a @ a / 2048.0
+    return a
+
+
+@pytest.mark.parametrize("third", ["null", "side"])
+def test_seed_table_across_streams_varying_k(third):
+    """The round-5 red case (gpurun_out/r05ag_pytest_gpu_k.log): two K = 100
+    rounds queued behind matmuls on streams sa / sb, then K = 1..79 rounds -- each a NEW seed table
+    and a new plan shape -- on a third stream (the null stream, or a side stream) while those two
+    still wait.  The context's seed-table ring keeps the tables the queued launches read, so all
+    81 outputs equal the oracle bit for bit."""
+    import torch
+    from flamingo_amd import MaskEngine
+    L, N = 4096, 2
+    with MaskEngine(0) as e:
+        e.set_tuning("small", 0)
+        rows, seeds, signs = rand_case(5151, N, 100, L)
+        d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+        d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+        sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+        sc = torch.cuda.Stream() if third == "side" else torch.cuda.default_stream()
+        torch.cuda.synchronize()
+        outs = []
+        for st in (sa, sb):
+            with torch.cuda.stream(st):
+                _queue_matmuls()
+                out = torch.empty(L, dtype=torch.int32, device="cuda")
+                e.aggregate_unmask_dev(d_rows, d_seeds[:100], d_signs[:100], out, L=L, stream=st)
+                outs.append(out)
+        later = []
+        with torch.cuda.stream(sc):
+            for K in range(1, 80):
+                out = torch.empty(L, dtype=torch.int32, device="cuda")
+                e.aggregate_unmask_dev(d_rows, d_seeds[:K], d_signs[:K], out, L=L, stream=sc)
+                later.append((K, out))
+        torch.cuda.synchronize()
+        want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+        for out in outs:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        for K, out in later:
+            want_k = O.aggregate_unmask(rows, seeds[:K], signs[:K], L=L, threads=8)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want_k), K
+
+
+def test_seed_table_ring_exhausted_across_streams():
+    """More streams with a queued round than the ring has tables (8): each stream's round gets its
+    own K, so a reused table must wait (on the device) for the queued reads of its previous seeds."""
+    import torch
+    from flamingo_amd import MaskEngine
+    L, N, S = 2048, 3, 11
+    with MaskEngine(0) as e:
+        e.set_tuning("small", 0)
+        rows, seeds, signs = rand_case(6262, N, 64, L)
+        d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+        d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+        streams = [torch.cuda.Stream() for _ in range(S)]
+        torch.cuda.synchronize()
+        outs = []
+        for i, st in enumerate(streams):
+            K = 64 - 5 * i
+            with torch.cuda.stream(st):
+                _queue_matmuls(6)
+                out = torch.empty(L, dtype=torch.int32, device="cuda")
+                e.aggregate_unmask_dev(d_rows, d_seeds[:K], d_signs[:K], out, L=L, stream=st)
+                outs.append((K, out))
+        torch.cuda.synchronize()
+        for K, out in outs:
+            want = O.aggregate_unmask(rows, seeds[:K], signs[:K], L=L, threads=8)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want), K
+
+
+def test_published_table_read_on_another_stream():
+    """flm_seed_table_dev on stream sa behind queued work, flm_aggregate_dev on stream sb at once:
+    the read waits for the table's write (its `written` event), with no ordering by the caller."""
+    import torch
+    from flamingo_amd import MaskEngine
+    L, N, K = 4096, 4, 40
+    with MaskEngine(0) as e:
+        rows, seeds, signs = rand_case(7373, N, K, L)
+        d_rows = torch.from_numpy(rows.view(np.int32)).cuda()
+        d_seeds, d_signs = torch.from_numpy(seeds).cuda(), torch.from_numpy(signs).cuda()
+        sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(sa):
+            _queue_matmuls()
+            e.seed_table_dev(d_seeds, d_signs, stream=sa)
+        out = torch.empty(L, dtype=torch.int32, device="cuda")
+        with torch.cuda.stream(sb):
+            e.aggregate_dev(d_rows, K, out, L=L, stream=sb)
+        torch.cuda.synchronize()
+        want = O.aggregate_unmask(rows, seeds, signs, L=L, threads=8)
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+
+
+def test_get_tuning_reads_the_context(eng):
+    """get_tuning reads the library (flm_get_tuning), so a value set through another wrapper of the
+    same context -- here a direct flm_set_tuning call -- is what it returns."""
+    assert eng.get_tuning("min_items") == 1024
+    assert eng.lib.flm_set_tuning(eng.ctx, b"min_items", 2048) == 0
+    try:
+        assert eng.get_tuning("min_items") == 2048
+    finally:
+        eng.set_tuning("min_items", 1024)
+    assert eng.get_tuning("pairing") == 1 and eng.get_tuning("ec_coop") == -1
+    with pytest.raises(RuntimeError, match="unknown tuning key"):
+        eng.get_tuning("ec_row_terms")
 
 
 def test_aggregate_wraps_mod_2_32(eng):

@@ -28,7 +28,6 @@ ap.add_argument("--scalars", choices=["random", "lagrange", "pow2"], default="ra
                 help="pow2: every lambda = 2^255 (one wNAF digit: ~258 doublings and no additions, to split the chain)")
 ap.add_argument("--coop", type=int, default=0, help="flm_set_tuning ec_coop (four waves per 64 products)")
 ap.add_argument("--terms", type=int, default=1, help="flm_set_tuning ec_terms (Straus: combine terms per lane)")
-ap.add_argument("--row-terms", type=int, default=1, help="flm_set_tuning ec_row_terms (Straus inside the row kernel)")
 ap.add_argument("--spread", type=int, default=0, help="flm_set_tuning ec_spread (KiB of LDS per EC workgroup)")
 ap.add_argument("--pick", default="first", choices=("first", "stride", "xcd_stride", "xcd"), help="which CUs --cus selects (pick_cus)")
 ap.add_argument("--cus", type=int, default=0, help="run on a CU-masked stream of this many CUs ('first' pick)")
@@ -51,7 +50,6 @@ eng.set_tuning("ec_threads", a.threads)
 eng.set_tuning("ec_coop", a.coop)
 eng.set_tuning("ec_terms", a.terms)
 eng.set_tuning("ec_spread", a.spread)
-eng.set_tuning("ec_row_terms", a.row_terms)
 c1_t = torch.from_numpy(c1).to(dev)
 sh_t = torch.from_numpy(shares).to(dev)
 lam_t = torch.from_numpy(C.scalars_to_wire(lams)).to(dev)

@@ -12,7 +12,7 @@
 #   sim          ABIDES simulations c1 (n=128) and n=1024 x 2 iterations -> TAG_sim_*.log
 #   simc3 / simc5 / simc5r   the agents at BASELINE c3, c5 (n=4096, L=2^20, 10 iterations, 1 % dropouts), reduced c5
 #   simprof      cProfile of the reduced c5 run;  simtrace  rocprofv3 kernel trace of a 4-iteration c5 run
-#   h2c          the hash-to-curve table launch under a kernel trace;  ecstraus  Straus-in-row EC measurements
+#   h2c          the hash-to-curve table launch under a kernel trace
 #   rccl         tools/rccl_clique_smoke.py (forced one-device RCCL clique + world-1 forced collectives),
 #                then the same with AMD_LOG_LEVEL=4: the kernels it dispatched (RCCL's included)
 #   rccltrace    the same script under rocprofv3 --kernel-trace --stats (put it last in a call)
@@ -76,17 +76,33 @@ for step in "$@"; do
         -o run -- python3 -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 4 --dropout 0.01 \
         --latency deterministic -k -s 5 > "$O/${TAG}_simtrace.log" 2>&1) || { tail -30 "$O/${TAG}_simtrace.log"; exit 1; }
       grep "iteration [0-9]*:" "$O/${TAG}_simtrace.log" ;;
-    ecstraus)
-      # the EC combine alone at one G = 8 rank's c5 share (D = 121, T = 20) with 1 / 2 / 4 terms per row chain,
-      # then one rank's shares -> final with the row kernel at each (tools/probes/rank8_overlap_probe.py --straus)
-      for g in 1 2 4; do
-        timeout -k 10 120 python tools/ec_bench.py --D 121 --T 20 --scalars lagrange --coop 2 --row-terms $g --reps 20 \
-          --cpu-sample 10 > "$O/${TAG}_ecbench_row$g.log" 2>&1 || { tail -20 "$O/${TAG}_ecbench_row$g.log"; exit 1; }
-        tail -1 "$O/${TAG}_ecbench_row$g.log" | cut -c1-300
+    stallab)
+      # the agent run's first-iteration unmask stall: c5 with 4 iterations, alternating
+      # the default allocator with glibc's mmap threshold pinned at 32 MiB and trimming off (freed numpy
+      # bodies then stay in the heap instead of being unmapped)
+      for v in base mmap base mmap; do
+        if [ $v = mmap ]; then envs="MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TRIM_THRESHOLD_=68719476736"; else envs=""; fi
+        env $envs timeout -k 10 300 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 4 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_stall_$v.log" 2>&1 || { tail -30 "$O/${TAG}_stall_$v.log"; exit 1; }
+        echo "== $v"; grep "iteration [0-9]*:" "$O/${TAG}_stall_$v.log" | sed 's/.*iteration/iteration/' | cut -c1-40,150-230
+        cat "$O/${TAG}_stall_$v.log" >> "$O/${TAG}_stall_all.txt"
+      done ;;
+    stallscr)
+      # the same c5 run (3 iterations) with ROCr's scratch reclaim off, two ways, then the default under a
+      # kernel + copy + scratch-memory trace (the EC kernels use scratch: is the stall a scratch reclaim?)
+      for v in noreclaim noasync noreclaim noasync; do
+        if [ $v = noreclaim ]; then envs="HSA_NO_SCRATCH_RECLAIM=1"; else envs="HSA_ENABLE_SCRATCH_ASYNC_RECLAIM=0"; fi
+        env $envs timeout -k 10 300 python -u -m flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 3 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_stall_$v.log" 2>&1 || { tail -30 "$O/${TAG}_stall_$v.log"; exit 1; }
+        echo "== $v"; grep -h "iteration [0-9]*:" "$O/${TAG}_stall_$v.log" | sed 's/.*iteration \([0-9]*\):.*unmask + D2H \(.*\)/it \1: \2/'
+        cat "$O/${TAG}_stall_$v.log" >> "$O/${TAG}_stall_all.txt"
       done
-      timeout -k 10 300 python -u tools/probes/rank8_overlap_probe.py --straus > "$O/${TAG}_rank8_straus.log" 2>&1 \
-        || { tail -20 "$O/${TAG}_rank8_straus.log"; exit 1; }
-      grep -v amdgpu.ids "$O/${TAG}_rank8_straus.log" ;;
+      (cd /tmp && PYTHONPATH="$R" timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --scratch-memory-trace \
+        --output-format csv -d "$O/${TAG}_scrtrace" -o run -- python3 -u -m flamingo_amd.abides -c flamingo -n 4096 \
+        --vector_len 1048576 -i 3 --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_scrtrace.log" 2>&1) \
+        || { tail -30 "$O/${TAG}_scrtrace.log"; exit 1; }
+      echo "== traced"; grep -h "iteration [0-9]*:" "$O/${TAG}_scrtrace.log" | sed 's/.*iteration \([0-9]*\):.*unmask + D2H \(.*\)/it \1: \2/'
+      find "$O/${TAG}_scrtrace" -name '*.csv' -exec gzip -f {} + ; true ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \

@@ -62,18 +62,8 @@ if "--row" in sys.argv:   # round 4: the row-field cooperative kernel (ec_coop 2
                         (f"cu_split_coop_{c}_items4096",
                          dict(ec_cus=c, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=1, pass1_min_items=4096), True)
                         for c in (72, 96)]
-row_terms = {}
-if "--straus" in sys.argv:   # round 5: Straus grouping inside the row kernel (ec_row_terms), unpartitioned
-    cases = [cases[0]]
-    for g in (1, 2, 4, 1, 2, 4):
-        cases.append((f"overlap_row_terms{g}", dict(), True))
-        row_terms[len(cases) - 1] = g
-    for g in (1, 4):
-        cases.append((f"cu_split_row_128_terms{g}",
-                      dict(ec_cus=128, cu_pick="first", pair_queue=True, ec_terms=1, ec_coop=2, pass1_min_items=4096), True))
-        row_terms[len(cases) - 1] = g
+# round 5's --straus cases (Straus inside the row kernel) were retired with ec_mul_row_straus_kernel (-3 %)
 for ci, (name, kw, ovl) in enumerate(cases):
-    eng.set_tuning("ec_row_terms", row_terms.get(ci, 1))
     rec = ServerReconstruction(eng, **kw)
     dst = ref if name == "sequential" else out
     args = (S, L8, t["lambdas"], t["mi_shares"], t["c1"], t["pair_shares"], t["pair_signs"], dst)
