@@ -136,8 +136,11 @@ int rccl_missing(flm_ctx *ctx) {
 
 namespace flm {
 // Finalize (flushes the communicator's outstanding operations and joins its proxy work) and then
-// destroy, with the context's device current.  Callers have synchronised the device first: the
-// collectives may have been enqueued on streams other than the context's own (a torch comm stream).
+// destroy, with the context's device current.  Callers synchronise the device first (flm_free and
+// flm_comm_destroy call hipDeviceSynchronize when a communicator is attached): the collectives may
+// have been enqueued on streams other than the context's own (a torch comm stream).  One process
+// per GPU: each rank finalizes its own communicator.  A one-thread clique goes through
+// comm_release_clique instead.
 void comm_release(flm_ctx *ctx) {
     CommState *cs = comm_of(ctx);
     if (!cs) return;
@@ -147,6 +150,37 @@ void comm_release(flm_ctx *ctx) {
     }
     delete cs;
     *flm::rt::comm_slot(ctx) = nullptr;
+}
+
+// A clique driven by one thread (ncclCommInitAll, flm_group): every device is synchronised, then
+// all members are finalized inside ONE group -- a member's finalize waits for the clique to be
+// quiescent, so finalizing them one after another from this thread could wait on members not yet
+// finalized -- and only then destroyed.  Without ncclCommFinalize (RCCL before 2.18) the members are
+// destroyed one by one, as NCCL's single-thread examples do.
+void comm_release_clique(flm_ctx *const *ctxs, int n) {
+    Rccl *r = rccl();
+    std::vector<CommState *> cs;
+    for (int q = 0; q < n; ++q)
+        if (CommState *c = comm_of(ctxs[q])) cs.push_back(c);
+    if (cs.empty()) return;
+    for (int q = 0; q < n; ++q) {
+        if (hipSetDevice(flm::rt::device_of(ctxs[q])) == hipSuccess) (void)hipDeviceSynchronize();
+        (void)hipGetLastError();
+    }
+    if (r && r->CommFinalize) {
+        (void)r->GroupStart();
+        for (CommState *c : cs)
+            if (c->comm) (void)r->CommFinalize(c->comm);
+        (void)r->GroupEnd();
+    }
+    for (int q = 0; q < n; ++q) {
+        CommState *c = comm_of(ctxs[q]);
+        if (!c) continue;
+        (void)hipSetDevice(flm::rt::device_of(ctxs[q]));
+        if (c->comm && r) (void)r->CommDestroy(c->comm);
+        delete c;
+        *flm::rt::comm_slot(ctxs[q]) = nullptr;
+    }
 }
 }  // namespace flm
 
@@ -453,6 +487,7 @@ int flm_group_init_flags(flm_group **out, int n, const int *devices, unsigned fl
 void flm_group_free(flm_group *g) {
     flm::rt::DeviceScope dev_scope_;  // the rank loops below switch devices
     if (!g) return;
+    if (g->clique) flm::comm_release_clique(g->ctx.data(), (int)g->ctx.size());  // before any flm_free
     for (int r = 0; r < (int)g->ctx.size(); ++r) {
         (void)hipSetDevice(g->dev[r]);
         (void)hipStreamSynchronize(flm::rt::stream_of(g->ctx[r]));

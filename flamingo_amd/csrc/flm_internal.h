@@ -99,6 +99,10 @@ uint32_t pair_units_count(int K, uint64_t L, uint32_t *n_tiles);
 hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *d_dst, uint64_t L, uint32_t *d_ws,
                              int groups, hipStream_t stream);
 hipError_t launch_flag_set(uint32_t *d_ws, hipStream_t stream);
+// d_out[k * pitch + l] = PRG(seed k)[16 ctr0 + l], l < L, k < K (prg_expand_kernel): `groups` one-wave
+// workgroups walk the K x ceil(L / 1024) units; mode bit 0 nontemporal stores, bit 1 LDS-staged stores.
+hipError_t launch_prg_expand(const SeedRec *d_recs, int K, uint64_t L, uint64_t pitch, uint32_t ctr0,
+                             uint32_t *d_out, int groups, int mode, hipStream_t stream);
 hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst, uint64_t n, hipStream_t stream);
 // dst[l] = sum_{g<G} d_parts[g][lo + l], l < n (G <= kMaxParts, all on the launching device).
 constexpr int kMaxParts = 16;
@@ -172,4 +176,7 @@ int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uin
                      int K, size_t L, size_t mask_lo, size_t mask_hi, uint32_t *d_out);
 }  // namespace rt
 void comm_release(flm_ctx *ctx);  // flm_comm.hip: drop the context's communicator (flm_free)
+// flm_comm.hip: synchronise every device, finalize a one-thread clique's members in one RCCL group,
+// then destroy them (flm_group_free)
+void comm_release_clique(flm_ctx *const *ctxs, int n);
 }  // namespace flm

@@ -126,6 +126,8 @@ struct SeedTable {
 
 // flm_last_plan's variant for a round run by small_round_kernel (items = its workgroups)
 constexpr int kSmallRoundVariant = 100;
+// flm_last_plan's variant after a PRG expansion by prg_expand_kernel (items = its workgroups)
+constexpr int kExpandVariant = 101;
 
 struct flm_ctx {
     int device = 0;
@@ -166,6 +168,9 @@ struct flm_ctx {
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
                              // 2 same-tile window items (plan_window_same; 0.228 vs 0.188 ms at G = 8, r02_ab_window_same.log)
+    int tune_expand_mode = 0;    // prg_expand_kernel stores: bit 0 nontemporal, bit 1 LDS-staged (coalesced)
+    int tune_expand_waves = 16;  // prg_expand_kernel one-wave workgroups per CU
+    int n_cus = 0;               // the device's CU count (flm_init)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
 
@@ -1112,6 +1117,10 @@ int flm_init(flm_ctx **out, int device) {
         delete ctx;
         return fail(nullptr, FLM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    if (hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->n_cus = 256;  // MI355X
+    }
     stage_prealloc(ctx);
     *out = ctx;
     return 0;
@@ -1357,10 +1366,34 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     if (pitch % 4 || pitch < round_up(L, 4)) return fail(ctx, FLM_EINVAL, "pitch must be a multiple of 4 and >= L");
     if ((uintptr_t)d_out & 15) return fail(ctx, FLM_EINVAL, "out must be 16-byte aligned");
     if (int rc = check_range(ctx, slot0 + L)) return rc;
+    if ((uint64_t)K * ((L + 1023) / 1024) > 0xFFFFFFFFull)
+        return fail(ctx, FLM_EINVAL, "K=%d x %zu slots: more than 2^32 1024-slot units", K, L);
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the HIP null stream
     FLM_ON_DEVICE(ctx);
-    // +1 signs are written into the staging slot with the work items: no host wait
-    return run_rows_jobs(ctx, nullptr, pitch, K, nullptr, nullptr, d_seeds, K, 0u, L, slot0, d_out, s);
+    // +1 signs through a staging slot (no host wait), the seed schedule, then prg_expand_kernel
+    int rc = 0;
+    StageSlot *slot = stage_acquire(ctx, (size_t)K, &rc);
+    if (!slot) return rc;
+    std::memset(slot->host, 1, (size_t)K);
+    FLM_HIP(ctx, stage_upload(slot, (size_t)K, s));
+    SeedTable *table = nullptr;
+    const int groups = std::max(1, ctx->n_cus * ctx->tune_expand_waves);
+    rc = run_seed_schedule(ctx, d_seeds, slot->dev.as<int8_t>(), K, s, &table);
+    if (!rc) {
+        hipError_t e = flm::launch_prg_expand(table->recs.as<SeedRec>(), K, L, pitch, (uint32_t)(slot0 / 16), d_out,
+                                              groups, ctx->tune_expand_mode, s);
+        if (e == hipSuccess) e = table_read(table, s);
+        if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "prg_expand launch: %s", hipGetErrorString(e));
+    }
+    // the slot is busy until the work enqueued so far has run, whether or not it all got enqueued
+    FLM_HIP(ctx, stage_commit(slot, s));
+    if (rc) return rc;
+    const uint64_t units = (uint64_t)K * ((L + 1023) / 1024);
+    ctx->last_items = (int)std::min<uint64_t>(units, (uint64_t)groups);
+    ctx->last_tile = flm::kWaveSlots;
+    ctx->last_atomics = 0;
+    ctx->last_variant = kExpandVariant;
+    return 0;
 }
 
 int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K, uint32_t *acc, size_t L,
@@ -1458,6 +1491,12 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "ec_coop") {
         if (value < -1 || value > 2) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0, 1 or 2");
         ctx->tune_ec_coop = value;
+    } else if (k == "expand_mode") {
+        if (value < 0 || value > 3) return fail(ctx, FLM_EINVAL, "expand_mode must be 0..3");
+        ctx->tune_expand_mode = value;
+    } else if (k == "expand_waves") {
+        if (value < 1 || value > 32) return fail(ctx, FLM_EINVAL, "expand_waves must be in [1, 32]");
+        ctx->tune_expand_waves = value;
     } else if (k == "ec_threads") {
         if (value != 64 && value != 128 && value != 256)
             return fail(ctx, FLM_EINVAL, "ec_threads must be 64, 128 or 256");
@@ -1476,7 +1515,8 @@ int flm_get_tuning(const flm_ctx *ctx, const char *key, int *value) {
         {"variant", ctx->tune_variant},       {"pairing", ctx->tune_pairing},     {"subtiles", ctx->tune_subtiles},
         {"ec_waves", ctx->tune_ec_waves},     {"small", ctx->tune_small},         {"min_items", ctx->tune_min_items},
         {"ec_spread", ctx->tune_ec_spread},   {"ec_terms", ctx->tune_ec_terms},   {"ec_coop", ctx->tune_ec_coop},
-        {"ec_threads", ctx->tune_ec_threads}};
+        {"ec_threads", ctx->tune_ec_threads}, {"expand_mode", ctx->tune_expand_mode},
+        {"expand_waves", ctx->tune_expand_waves}};
     for (const auto &kv : knobs)
         if (k == kv.first) {
             *value = kv.second;

@@ -72,6 +72,35 @@ def test_prg_expand_batch_vs_oracle(eng):
             assert np.array_equal(got[k], O.prg(seeds[k].tobytes(), L)), (k, L)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_prg_expand_dev_kernel_forms(eng, mode):
+    """prg_expand_kernel in every store form (expand_mode: bit 0 nontemporal, bit 1 LDS-staged) and
+    with a grid smaller than the unit count (grid-stride): ragged L (tails inside a 16-word block,
+    inside a 1024-slot chunk), PRG windows (slot0), a padded pitch that must stay untouched, and the
+    whole output against oracle.prg (SA_ServiceAgent.py:596-603)."""
+    import torch
+    g = rng(40 + mode)
+    eng.set_tuning("expand_mode", mode)
+    try:
+        for L, slot0, pad, waves in ((1, 0, 4, 16), (17, 16, 0, 16), (1023, 4096, 8, 1), (1025, 0, 4, 2),
+                                     (5000, 2**20 - 5008, 12, 16), (40000, 2**30, 0, 32)):
+            eng.set_tuning("expand_waves", waves)
+            K = int(g.integers(1, 40))
+            seeds = g.integers(0, 256, size=(K, 32), dtype=np.uint8)
+            pitch = (L + 3) // 4 * 4 + pad
+            out = torch.full((K, pitch), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+            eng.prg_expand_dev(torch.from_numpy(seeds).cuda(), out, L, slot0=slot0)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint32)
+            for k in range(K):
+                assert np.array_equal(got[k, :L], O.prg(seeds[k].tobytes(), L, slot0)), (mode, L, slot0, k)
+            assert np.all(got[:, L:] == 0x3C3C3C3C), (mode, L, "wrote past L")
+            assert eng.last_plan()["variant"] == 101
+    finally:
+        eng.set_tuning("expand_mode", 0)
+        eng.set_tuning("expand_waves", 16)
+
+
 def test_keystream_golden(eng, golden):
     for e in golden["keystream"]:
         key, data = bytes.fromhex(e["key"]), bytes.fromhex(e["data"])

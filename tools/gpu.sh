@@ -103,6 +103,26 @@ for step in "$@"; do
         || { tail -30 "$O/${TAG}_scrtrace.log"; exit 1; }
       echo "== traced"; grep -h "iteration [0-9]*:" "$O/${TAG}_scrtrace.log" | sed 's/.*iteration \([0-9]*\):.*unmask + D2H \(.*\)/it \1: \2/'
       find "$O/${TAG}_scrtrace" -name '*.csv' -exec gzip -f {} + ; true ;;
+    stallnuma)
+      # is the stall a KFD queue eviction from an MMU-notifier invalidation of a pinned (userptr) buffer,
+      # e.g. by automatic NUMA balancing?  The kernel's settings, then c5 (3 iterations) alternating the
+      # default with MPOL_LOCAL (no NUMA-balancing scans of this process: tools/probes/mempolicy_run.py)
+      for f in /proc/sys/kernel/numa_balancing /sys/kernel/mm/transparent_hugepage/enabled \
+               /sys/kernel/mm/transparent_hugepage/defrag /proc/sys/kernel/numa_balancing_scan_delay_ms \
+               /proc/sys/kernel/numa_balancing_scan_period_min_ms; do echo "$f: $(cat $f 2>&1)"; done
+      grep -h "numa_\|thp_\|pgmigrate" /proc/vmstat 2>/dev/null | head -20 > "$O/${TAG}_vmstat_before.txt"
+      for v in local base local base local local; do
+        if [ $v = local ]; then pre="tools/probes/mempolicy_run.py"; else pre="-m"; fi
+        timeout -k 10 300 python -u $pre flamingo_amd.abides -c flamingo -n 4096 --vector_len 1048576 -i 3 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_stall_$v.log" 2>&1 || { tail -30 "$O/${TAG}_stall_$v.log"; exit 1; }
+        echo "== $v"; grep -h "iteration [0-9]*:" "$O/${TAG}_stall_$v.log" | sed 's/.*iteration \([0-9]*\):.*unmask + D2H \(.*\)/it \1: \2/'
+        cat "$O/${TAG}_stall_$v.log" >> "$O/${TAG}_stall_all.txt"
+      done
+      grep -h "numa_\|thp_\|pgmigrate" /proc/vmstat 2>/dev/null | head -20 > "$O/${TAG}_vmstat_after.txt"; true ;;
+    expand)
+      timeout -k 10 300 python -u tools/probes/expand_probe.py > "$O/${TAG}_expand_probe.log" 2>&1 \
+        || { tail -30 "$O/${TAG}_expand_probe.log"; exit 1; }
+      cat "$O/${TAG}_expand_probe.log" | grep -v amdgpu.ids ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \

@@ -16,3 +16,6 @@ cd $R && python3 tools/summarize_profile.py gpurun_out/prof_${TAG}_summary.json 
 # seed recovery (c5 shape): kernel trace + stats of tools/recovery_bench.py
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_recovery -o run -- python3 $R/tools/recovery_bench.py > $R/gpurun_out/prof_${TAG}_recovery.log 2>&1 || exit $?
+# standalone mask expansion (flm_prg_expand_dev, c5's D seeds x 2^20): kernel trace + stats, then its write traffic
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_expand -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_${TAG}_expand_pmc -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand_pmc.log 2>&1 || exit $?
