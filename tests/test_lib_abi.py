@@ -69,4 +69,13 @@ def test_round5_entry_points_reject_null_handles(lib):
     assert lib.flm_hash_to_curve_decimal_dev(None, 0, 1, None, None, None) == -1
     ms = ctypes.c_float()
     assert lib.flm_store_unmask_ms(None, ctypes.byref(ms)) == -1
-    assert b"0.3" in lib.flm_version()
+    assert b"0.4" in lib.flm_version()
+
+
+def test_round6_entry_points_reject_null_handles(lib):
+    """flm_get_tuning (round 6): a NULL context, key or output is an FLM_EINVAL with a message,
+    before any device call; the expansion knobs are refused on a NULL context too."""
+    v = ctypes.c_int(7)
+    assert lib.flm_get_tuning(None, b"pairing", ctypes.byref(v)) == -1 and b"NULL" in lib.flm_last_error(None)
+    assert v.value == 7
+    assert lib.flm_set_tuning(None, b"expand_mode", 1) == -1
