@@ -1071,8 +1071,9 @@ def measure_prg_expand(eng, torch, stream, ceil_gwords=None, K=PRG_EXPAND_K, L=1
     gw = words / (ms * 1e-3) / 1e9
     res = {"what": f"flm_prg_expand_dev: {K} pair seeds (c5's D) x L = {L} slots into device memory, one mask "
                    f"row per seed, median of {reps} launches (SA_ServiceAgent.py:596-603)",
-           "K": K, "L": L, "kernel": "items_kernel<16> (one wave per 1024 slots of one seed)",
-           "items": plan["items"], "kernel_ms": round(ms, 4), "kernel_ms_all": [round(t, 4) for t in times],
+           "K": K, "L": L, "kernel": "prg_expand_kernel (one-wave workgroups, runs of (seed, 1024-slot) units, "
+                                     "LDS-staged 1 KiB-contiguous stores)",
+           "workgroups": plan["items"], "note": "kernel_ms = seed schedule + expansion launch (HIP events around the call)", "kernel_ms": round(ms, 4), "kernel_ms_all": [round(t, 4) for t in times],
            "bytes_written_per_launch": int(4 * words), "GB/s_written": round(gbs, 1),
            "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "mask_gwords_per_s": round(gw, 1),
            "checked_against_oracle": {"match": ok, "rows": [0, K // 2, K - 1], "windows": [[0, n], [L - n, n]]}}

@@ -100,9 +100,9 @@ hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *
                              int groups, hipStream_t stream);
 hipError_t launch_flag_set(uint32_t *d_ws, hipStream_t stream);
 // d_out[k * pitch + l] = PRG(seed k)[16 ctr0 + l], l < L, k < K (prg_expand_kernel): `groups` one-wave
-// workgroups walk the K x ceil(L / 1024) units; mode bit 0 nontemporal stores, bit 1 LDS-staged stores.
+// workgroups take contiguous runs of the K x ceil(L / 1024) seed-major units.
 hipError_t launch_prg_expand(const SeedRec *d_recs, int K, uint64_t L, uint64_t pitch, uint32_t ctr0,
-                             uint32_t *d_out, int groups, int mode, hipStream_t stream);
+                             uint32_t *d_out, int groups, hipStream_t stream);
 hipError_t launch_add2(const uint32_t *d_a, const uint32_t *d_b, uint32_t *d_dst, uint64_t n, hipStream_t stream);
 // dst[l] = sum_{g<G} d_parts[g][lo + l], l < n (G <= kMaxParts, all on the launching device).
 constexpr int kMaxParts = 16;

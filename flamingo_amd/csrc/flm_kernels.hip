@@ -781,57 +781,50 @@ __global__ void flag_set_kernel(uint32_t *__restrict__ ws) {
 // ---------------------------------------------------------------- mask expansion
 // Standalone PRG expansion (north_star (i); the cancel_vec idiom of SA_ServiceAgent.py:596-603 and
 // SA_ClientAgent.py:248-250 for a whole batch of seeds): out[k * pitch + l] = PRG(seed k)[slot0 + l]
-// for l < L.  A unit is (seed k, 1024-slot chunk); one-wave workgroups walk the units grid-stride,
-// consecutive units being adjacent chunks of one seed's row.  Lane t makes ChaCha block
-// ctr0 + 64 chunk + t (slots 16t..16t+15 of the chunk) from the seed's SeedRec (scalar loads).
-//   LDS_STAGE: the 16 words go through the wave's 4 KiB of LDS and come back in coalesced order, so
-//              each 16-B store instruction writes 1 KiB contiguous (lane t: slot 4t + 256j);
-//   else       each lane stores its own 64 B (four 16-B stores at 64-B lane stride).
-//   NT:        nontemporal stores (the masks are written once and not read back by this kernel).
-// A wave's whole working set is one block (~40 VGPRs), so the grid is sized for occupancy, not units.
-template <bool LDS_STAGE, bool NT>
+// for l < L.  A unit is (seed k, 1024-slot chunk), numbered seed-major; one-wave workgroup g takes
+// the contiguous run of units [g U / G, (g + 1) U / G), so it loads a seed's SeedRec once (scalar
+// registers) for all of that seed's chunks in its run and writes consecutive 4 KiB of its row.
+// Lane t makes ChaCha block ctr0 + 64 chunk + t (slots 16t..16t+15 of the chunk); the 16 words
+// go through the wave's 4 KiB of LDS and come back in coalesced order, so each 16-B store
+// instruction writes 1 KiB contiguous (lane t: slot 4t + 256j).  Measured against storing each
+// lane's own 64 B (four 16-B stores at a 64-B lane stride): 1.45 vs 1.53 ms at K = 962, L = 2^20,
+// and nontemporal forms the same (LDS-staged) or 4.5x slower (lane-strided partial lines;
+// profiles/r06_expand_probe.log).  ~36 VGPRs: the grid is sized for occupancy (flm_set_tuning
+// "expand_waves"), not for the unit count.
 __global__ __launch_bounds__(64) void prg_expand_kernel(const SeedRec *__restrict__ recs, uint32_t chunks,
                                                         uint32_t n_units, uint64_t L, uint64_t pitch, uint32_t ctr0,
                                                         uint32_t *__restrict__ out) {
     __shared__ u32x4 lds[256];
     const int lane = threadIdx.x;
-    auto put = [&](uint32_t *dst, const u32x4 &v) {
-        if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(dst));
-        else *reinterpret_cast<u32x4 *>(dst) = v;
-    };
-    auto put_tail = [&](uint32_t *dst, const u32x4 &v, int n) {  // n < 4 valid words
-        if (n > 0) dst[0] = v.x;
-        if (n > 1) dst[1] = v.y;
-        if (n > 2) dst[2] = v.z;
-    };
-    for (uint32_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-        const uint32_t k = u / chunks, chunk = u - k * chunks;
-        uint32_t m[16];
+    const uint32_t u0 = (uint32_t)(((uint64_t)n_units * blockIdx.x) / gridDim.x);
+    const uint32_t u1 = (uint32_t)(((uint64_t)n_units * (blockIdx.x + 1)) / gridDim.x);
+    for (uint32_t u = u0; u < u1;) {
+        const uint32_t k = u / chunks;
+        const uint32_t end = min(u1, (k + 1) * chunks);
+        const SeedRec rec = recs[k];  // wave-uniform: scalar loads, once per seed of the run
+        uint32_t *row = out + (uint64_t)k * pitch;
+        for (uint32_t chunk = u - k * chunks; u < end; ++u, ++chunk) {
+            uint32_t m[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) m[i] = 0u;
-        chacha_mask_add(recs + k, ctr0 + chunk * 64u + (uint32_t)lane, m);
-        const int valid = (int)min<uint64_t>(1024u, L - (uint64_t)chunk * 1024u);
-        uint32_t *row = out + (uint64_t)k * pitch + (uint64_t)chunk * 1024u;
-        const u32x4 q[4] = {u32x4{m[0], m[1], m[2], m[3]}, u32x4{m[4], m[5], m[6], m[7]},
-                            u32x4{m[8], m[9], m[10], m[11]}, u32x4{m[12], m[13], m[14], m[15]}};
-        if constexpr (LDS_STAGE) {
-            __syncthreads();  // one wave per workgroup: the previous unit's reads are done
+            for (int i = 0; i < 16; ++i) m[i] = 0u;
+            chacha_mask_add(&rec, ctr0 + chunk * 64u + (uint32_t)lane, m);
+            const int valid = (int)min<uint64_t>(1024u, L - (uint64_t)chunk * 1024u);
+            uint32_t *dst = row + (uint64_t)chunk * 1024u;
+            __syncthreads();  // one wave per workgroup: the previous chunk's reads are done
 #pragma unroll
-            for (int j = 0; j < 4; ++j) lds[4 * lane + j] = q[j];
+            for (int j = 0; j < 4; ++j) lds[4 * lane + j] = u32x4{m[4 * j], m[4 * j + 1], m[4 * j + 2], m[4 * j + 3]};
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int slot = 4 * (lane + 64 * j);
                 const u32x4 v = lds[lane + 64 * j];
-                if (slot + 4 <= valid) put(row + slot, v);
-                else put_tail(row + slot, v, valid - slot);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int slot = 16 * lane + 4 * j;
-                if (slot + 4 <= valid) put(row + slot, q[j]);
-                else put_tail(row + slot, q[j], valid - slot);
+                if (slot + 4 <= valid) {
+                    *reinterpret_cast<u32x4 *>(dst + slot) = v;
+                } else {
+                    if (slot + 0 < valid) dst[slot + 0] = v.x;
+                    if (slot + 1 < valid) dst[slot + 1] = v.y;
+                    if (slot + 2 < valid) dst[slot + 2] = v.z;
+                }
             }
         }
     }
@@ -989,22 +982,13 @@ hipError_t launch_pair_units(bool side, const SeedRec *d_recs, int K, uint32_t *
 }
 
 hipError_t launch_prg_expand(const SeedRec *d_recs, int K, uint64_t L, uint64_t pitch, uint32_t ctr0,
-                             uint32_t *d_out, int groups, int mode, hipStream_t stream) {
+                             uint32_t *d_out, int groups, hipStream_t stream) {
     const uint64_t chunks = (L + 1023) / 1024, units = chunks * (uint64_t)K;
     if (K <= 0 || L == 0) return hipSuccess;
     if (units > 0xFFFFFFFFull || groups <= 0) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<uint64_t>(units, (uint64_t)groups);
-#define FLM_PE(LS, NT)                                                                                    \
-    hipLaunchKernelGGL((prg_expand_kernel<LS, NT>), dim3(grid), dim3(64), 0, stream, d_recs, (uint32_t)chunks, \
-                       (uint32_t)units, L, pitch, ctr0, d_out)
-    switch (mode) {
-        case 0: FLM_PE(false, false); break;
-        case 1: FLM_PE(false, true); break;
-        case 2: FLM_PE(true, false); break;
-        case 3: FLM_PE(true, true); break;
-        default: return hipErrorInvalidValue;
-    }
-#undef FLM_PE
+    hipLaunchKernelGGL(prg_expand_kernel, dim3(grid), dim3(64), 0, stream, d_recs, (uint32_t)chunks, (uint32_t)units,
+                       L, pitch, ctr0, d_out);
     return hipGetLastError();
 }
 

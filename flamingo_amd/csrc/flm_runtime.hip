@@ -107,16 +107,19 @@ using PlanKey = std::tuple<int, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t
 // its sign counts (meta), read by items_kernel / pair_units_kernel.  A context keeps a ring of
 // them so that a call on one stream never rewrites a table that launches queued on other streams
 // still read (the r05 cross-stream hazard): each table records its write
-// (`written`, on `w_stream`) and its last read on every stream (`readers`).  A table is rebuilt on
-// stream s only once every read and write of it on other streams has completed; when all
-// kSeedTables tables are still in use elsewhere, s waits on the device for the least recently used
-// one's events (hipStreamWaitEvent, never a host wait).  Reads on the writing stream are in order
-// by construction; a read on another stream (a published table used by flm_aggregate_dev there)
-// waits for `written` first.
+// stream (`w_stream`) and its last read on every stream (`readers`: one reused event per stream).
+// A write followed at once by a read on the same stream (every fused call) is covered by that read's
+// event; only a published table (flm_seed_table_dev: its reads may come on other streams) records
+// `written` itself -- one event record per call on the hot path.  A table is rebuilt on stream s
+// only once every read and write of it on other streams has completed; when all kSeedTables tables
+// are still in use elsewhere, s waits on the device for the least recently used one's events
+// (hipStreamWaitEvent, never a host wait).  Reads on the writing stream are in order by
+// construction; a read on another stream waits for `written` first.
 constexpr size_t kSeedTables = 8;
 struct SeedTable {
     DevBuf recs, meta;
     hipEvent_t written = nullptr;
+    bool written_valid = false;  // `written` was recorded after the last write (else a read on w_stream covers it)
     hipStream_t w_stream = nullptr;
     std::vector<std::pair<hipStream_t, hipEvent_t>> readers;
     uint64_t last_use = 0;
@@ -137,6 +140,8 @@ struct flm_ctx {
     std::vector<SeedTable *> tables;  // ring of device seed tables (SeedTable)
     SeedTable *cur_table = nullptr;   // the table the last seed-schedule / small-round launch wrote
     SeedTable *pub_table = nullptr;   // the table flm_seed_table_dev published for flm_aggregate_dev
+    DevBuf small_meta;                // sign counts of the one-launch small round (no seed table)
+    bool last_small = false;          // the last sign counts came from a small round (flm_check_signs)
     uint64_t table_clock = 0;
     std::vector<StageSlot *> slots;  // staging pool of the *_dev uploads (StageSlot)
     uint64_t slot_clock = 0;
@@ -168,8 +173,9 @@ struct flm_ctx {
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
                              // 2 same-tile window items (plan_window_same; 0.228 vs 0.188 ms at G = 8, r02_ab_window_same.log)
-    int tune_expand_mode = 0;    // prg_expand_kernel stores: bit 0 nontemporal, bit 1 LDS-staged (coalesced)
-    int tune_expand_waves = 16;  // prg_expand_kernel one-wave workgroups per CU
+    int tune_expand_waves = 64;  // prg_expand_kernel one-wave workgroups per CU: 16 / 32 / 64 -> 1.57 / 1.43 / 1.38 ms
+                                 // at K = 962, L = 2^20 (profiles/r06_expand_probe_waves.log); ~9 fit a SIMD at once,
+                                 // the rest queue behind them and even out the runs' ends
     int n_cus = 0;               // the device's CU count (flm_init)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
@@ -685,7 +691,7 @@ bool event_done(hipEvent_t e) {
 
 // No read or write of `t` on a stream other than s is still pending: s may rewrite it at once.
 bool table_free_on(const SeedTable *t, hipStream_t s) {
-    if (t->w_stream != s && !event_done(t->written)) return false;
+    if (t->w_stream != s && t->written_valid && !event_done(t->written)) return false;
     for (const auto &r : t->readers)
         if (r.first != s && !event_done(r.second)) return false;
     return true;
@@ -711,7 +717,7 @@ SeedTable *table_acquire(flm_ctx *ctx, int K, size_t meta_words, hipStream_t s, 
         for (SeedTable *c : ctx->tables)
             if (c->last_use < t->last_use) t = c;
         hipError_t e = hipSuccess;
-        if (t->w_stream != s) e = hipStreamWaitEvent(s, t->written, 0);
+        if (t->w_stream != s && t->written_valid) e = hipStreamWaitEvent(s, t->written, 0);
         for (const auto &r : t->readers)
             if (e == hipSuccess && r.first != s) e = hipStreamWaitEvent(s, r.second, 0);
         if (e != hipSuccess) {
@@ -735,17 +741,29 @@ SeedTable *table_acquire(flm_ctx *ctx, int K, size_t meta_words, hipStream_t s, 
     return t;
 }
 
-// The table's write launch has been enqueued on s.
-hipError_t table_written(flm_ctx *ctx, SeedTable *t, hipStream_t s) {
+// The table's write launch has been enqueued on s.  record: mark it with `written` (a published
+// table); otherwise the caller's read launch on s follows and table_read() covers both -- or, when
+// the read cannot be enqueued, table_cover() records `written` after all.
+hipError_t table_written(flm_ctx *ctx, SeedTable *t, hipStream_t s, bool record) {
     t->w_stream = s;
+    t->written_valid = record;
     ctx->cur_table = t;
-    return hipEventRecord(t->written, s);
+    ctx->last_small = false;
+    return record ? hipEventRecord(t->written, s) : hipSuccess;
+}
+
+void table_cover(SeedTable *t, hipStream_t s) {
+    if (t && !t->written_valid && hipEventRecord(t->written, s) == hipSuccess) t->written_valid = true;
+    (void)hipGetLastError();
 }
 
 // Before a launch on s that reads t: order it after t's write when that ran on another stream.
 hipError_t table_before_read(SeedTable *t, hipStream_t s) {
-    if (t->w_stream == s || event_done(t->written)) return hipSuccess;
-    return hipStreamWaitEvent(s, t->written, 0);
+    if (t->w_stream == s) return hipSuccess;
+    if (t->written_valid) return event_done(t->written) ? hipSuccess : hipStreamWaitEvent(s, t->written, 0);
+    for (const auto &r : t->readers)  // (not reached: a write recorded no event only when a read followed)
+        if (r.first == t->w_stream) return hipStreamWaitEvent(s, r.second, 0);
+    return hipSuccess;
 }
 
 // A launch that reads t has been enqueued on s: record it as the table's last read on s (one event
@@ -773,7 +791,7 @@ hipError_t table_read(SeedTable *t, hipStream_t s) {
 }
 
 void table_free(SeedTable *t) {
-    if (t->written) (void)hipEventSynchronize(t->written);
+    if (t->written && t->written_valid) (void)hipEventSynchronize(t->written);
     for (auto &r : t->readers) (void)hipEventSynchronize(r.second);
     t->recs.release();
     t->meta.release();
@@ -782,17 +800,18 @@ void table_free(SeedTable *t) {
     delete t;
 }
 
-// The one-launch small round writes its sign counts into a seed table's meta (flm_check_signs)
-// and builds no records, so it unpublishes the table like every other rebuild.
+// The one-launch small round builds no seed table: it reads the raw seeds and only WRITES its sign
+// counts, into a buffer of its own (flm_check_signs reads them; small rounds racing on several
+// streams can only race on that diagnostic, never on a sum).  It unpublishes the table like every
+// other entry point that takes seeds, so flm_aggregate_dev cannot pair with its seeds.  No event:
+// c2's whole round is ~7 us of host time.
 int run_small_round(flm_ctx *ctx, int B, const uint32_t *d_rows, uint64_t pitch, int N, const uint8_t *d_seeds,
                     const int8_t *d_signs, int K, uint64_t L, uint64_t mask_lo, uint64_t mask_hi, uint64_t prg_slot0,
                     uint32_t *d_out, hipStream_t s) {
-    int rc = 0;
-    SeedTable *t = table_acquire(ctx, 0, 4, s, &rc);
-    if (!t) return rc;
+    FLM_HIP(ctx, ctx->small_meta.reserve(4 * sizeof(uint32_t)));
     FLM_HIP(ctx, flm::launch_small_round(B, d_rows, pitch, N, d_seeds, d_signs, K, L, mask_lo, mask_hi,
-                                         (uint32_t)(prg_slot0 / 16), d_out, t->meta.as<uint32_t>(), s));
-    FLM_HIP(ctx, table_written(ctx, t, s));
+                                         (uint32_t)(prg_slot0 / 16), d_out, ctx->small_meta.as<uint32_t>(), s));
+    ctx->last_small = true;
     ctx->pub_table = nullptr;
     ctx->table_k = -1;
     return 0;
@@ -810,9 +829,13 @@ int run_seed_schedule(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sign
     int rc = 0;
     SeedTable *t = table_acquire(ctx, K, 2 + 2 * (size_t)groups, s, &rc);
     if (!t) return rc;
-    FLM_HIP(ctx, flm::launch_seed_schedule(d_seeds, d_signs, K, t->recs.as<SeedRec>(), t->meta.as<uint32_t>(), s,
-                                           zero_out, zero_n));
-    FLM_HIP(ctx, table_written(ctx, t, s));
+    const hipError_t e = flm::launch_seed_schedule(d_seeds, d_signs, K, t->recs.as<SeedRec>(), t->meta.as<uint32_t>(),
+                                                   s, zero_out, zero_n);
+    if (e != hipSuccess) {
+        table_cover(t, s);  // whatever part of it got enqueued
+        return fail(ctx, FLM_EHIP, "seed schedule launch: %s", hipGetErrorString(e));
+    }
+    FLM_HIP(ctx, table_written(ctx, t, s, /*record=*/publish));
     ctx->pub_table = publish ? t : nullptr;
     ctx->table_k = publish ? K : -1;
     *out = t;
@@ -1053,6 +1076,7 @@ int run_rows_jobs(flm_ctx *ctx, const uint32_t *d_x, uint64_t pitch, int N, cons
         if (e == hipSuccess) e = table_read(table, s);
         if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "items launch: %s", hipGetErrorString(e));
     }
+    if (table && (rc || !plan.n_items)) table_cover(table, s);  // no read recorded after the table's write
     // the slot is busy until the work enqueued so far has run, whether or not it all got enqueued
     FLM_HIP(ctx, stage_commit(slot, s));
     if (rc) return rc;
@@ -1137,6 +1161,8 @@ void flm_free(flm_ctx *ctx) {
     for (StageSlot *s : ctx->slots) (void)hipEventSynchronize(s->done);  // launches on other streams
     for (auto &kv : ctx->plans) plan_free(kv.second);
     for (SeedTable *t : ctx->tables) table_free(t);  // waits for the table's readers on every stream
+    if (ctx->small_meta.p) (void)hipDeviceSynchronize();  // small rounds on any stream may still write it
+    ctx->small_meta.release();
     for (DevBuf *b : {&ctx->rows, &ctx->out, &ctx->seeds, &ctx->signs, &ctx->bytes_in, &ctx->bytes_out, &ctx->ec_in,
                       &ctx->ec_base, &ctx->ec_scal, &ctx->ec_jac, &ctx->ec_out, &ctx->ec_dig, &ctx->ec_flags})
         b->release();
@@ -1256,7 +1282,8 @@ int flm_aggregate_unmask_dev(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pi
     // two submissions: seed schedule (+ the zero-fill an atomics plan needs), then the items
     SeedTable *table = nullptr;
     if ((rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, &table, plan->needs_zero ? d_out : nullptr, L))) return rc;
-    return run_plan(ctx, *plan, table, d_rows, row_pitch, d_out, L, s, plan->needs_zero);
+    if ((rc = run_plan(ctx, *plan, table, d_rows, row_pitch, d_out, L, s, plan->needs_zero))) table_cover(table, s);
+    return rc;
 }
 
 int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, const uint8_t *seeds,
@@ -1381,9 +1408,10 @@ int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, ui
     rc = run_seed_schedule(ctx, d_seeds, slot->dev.as<int8_t>(), K, s, &table);
     if (!rc) {
         hipError_t e = flm::launch_prg_expand(table->recs.as<SeedRec>(), K, L, pitch, (uint32_t)(slot0 / 16), d_out,
-                                              groups, ctx->tune_expand_mode, s);
+                                              groups, s);
         if (e == hipSuccess) e = table_read(table, s);
         if (e != hipSuccess) rc = fail(ctx, FLM_EHIP, "prg_expand launch: %s", hipGetErrorString(e));
+        if (rc) table_cover(table, s);
     }
     // the slot is busy until the work enqueued so far has run, whether or not it all got enqueued
     FLM_HIP(ctx, stage_commit(slot, s));
@@ -1491,11 +1519,8 @@ int flm_set_tuning(flm_ctx *ctx, const char *key, int value) {
     } else if (k == "ec_coop") {
         if (value < -1 || value > 2) return fail(ctx, FLM_EINVAL, "ec_coop must be -1, 0, 1 or 2");
         ctx->tune_ec_coop = value;
-    } else if (k == "expand_mode") {
-        if (value < 0 || value > 3) return fail(ctx, FLM_EINVAL, "expand_mode must be 0..3");
-        ctx->tune_expand_mode = value;
     } else if (k == "expand_waves") {
-        if (value < 1 || value > 32) return fail(ctx, FLM_EINVAL, "expand_waves must be in [1, 32]");
+        if (value < 1 || value > 256) return fail(ctx, FLM_EINVAL, "expand_waves must be in [1, 256]");
         ctx->tune_expand_waves = value;
     } else if (k == "ec_threads") {
         if (value != 64 && value != 128 && value != 256)
@@ -1515,8 +1540,7 @@ int flm_get_tuning(const flm_ctx *ctx, const char *key, int *value) {
         {"variant", ctx->tune_variant},       {"pairing", ctx->tune_pairing},     {"subtiles", ctx->tune_subtiles},
         {"ec_waves", ctx->tune_ec_waves},     {"small", ctx->tune_small},         {"min_items", ctx->tune_min_items},
         {"ec_spread", ctx->tune_ec_spread},   {"ec_terms", ctx->tune_ec_terms},   {"ec_coop", ctx->tune_ec_coop},
-        {"ec_threads", ctx->tune_ec_threads}, {"expand_mode", ctx->tune_expand_mode},
-        {"expand_waves", ctx->tune_expand_waves}};
+        {"ec_threads", ctx->tune_ec_threads}, {"expand_waves", ctx->tune_expand_waves}};
     for (const auto &kv : knobs)
         if (k == kv.first) {
             *value = kv.second;
@@ -1528,16 +1552,20 @@ int flm_get_tuning(const flm_ctx *ctx, const char *key, int *value) {
 int flm_check_signs(flm_ctx *ctx, int *bad_count) {
     if (!ctx || !bad_count) return fail(ctx, FLM_EINVAL, "NULL argument");
     *bad_count = 0;
-    const SeedTable *t = ctx->cur_table;
-    if (!t) return 0;
+    const SeedTable *t = ctx->last_small ? nullptr : ctx->cur_table;
+    const DevBuf *meta = ctx->last_small ? &ctx->small_meta : (t ? &t->meta : nullptr);
+    if (!meta || !meta->p) return 0;
     FLM_ON_DEVICE(ctx);
-    FLM_HIP(ctx, hipEventSynchronize(t->written));
+    if (t && t->written_valid) FLM_HIP(ctx, hipEventSynchronize(t->written));
+    if (t)
+        for (const auto &r : t->readers)
+            if (r.first == t->w_stream) FLM_HIP(ctx, hipEventSynchronize(r.second));
     uint32_t parts = 0;
-    FLM_HIP(ctx, hipMemcpy(&parts, t->meta.p, sizeof parts, hipMemcpyDeviceToHost));
-    if (2 + 2 * (size_t)parts > t->meta.cap / sizeof(uint32_t))
+    FLM_HIP(ctx, hipMemcpy(&parts, meta->p, sizeof parts, hipMemcpyDeviceToHost));
+    if (2 + 2 * (size_t)parts > meta->cap / sizeof(uint32_t))
         return fail(ctx, FLM_EHIP, "seed table sign counts: %u parts overrun the table", parts);
     std::vector<uint32_t> m(2 + 2 * (size_t)parts);
-    FLM_HIP(ctx, hipMemcpy(m.data(), t->meta.p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    FLM_HIP(ctx, hipMemcpy(m.data(), meta->p, m.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     for (uint32_t p = 0; p < parts; ++p) *bad_count += (int)m[3 + 2 * p];
     return 0;
 }
@@ -1663,8 +1691,12 @@ int flm_pair_units_dev(flm_ctx *ctx, const uint8_t *d_seeds, const int8_t *d_sig
     if (L == 0 || K == 0) return 0;
     SeedTable *table = nullptr;
     if (int rc = run_seed_schedule(ctx, d_seeds, d_signs, K, s, &table)) return rc;
-    FLM_HIP(ctx, flm::launch_pair_units(!final_pass, table->recs.as<flm::SeedRec>(), K, d_dst, L, d_ws, groups, s));
-    FLM_HIP(ctx, table_read(table, s));
+    hipError_t e = flm::launch_pair_units(!final_pass, table->recs.as<flm::SeedRec>(), K, d_dst, L, d_ws, groups, s);
+    if (e == hipSuccess) e = table_read(table, s);
+    if (e != hipSuccess) {
+        table_cover(table, s);
+        return fail(ctx, FLM_EHIP, "pair units launch: %s", hipGetErrorString(e));
+    }
     return 0;
 }
 

@@ -186,10 +186,9 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              runs cooperatively.
  *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
  *              per-lane combine kernels (caps their workgroups per CU).
- *   "expand_mode" 0..3 (default 0): stores of the expansion kernel (flm_prg_expand[_dev]):
- *              bit 0 nontemporal, bit 1 staged through LDS into 1 KiB-contiguous stores.
- *   "expand_waves" 1..32 (default 16): its one-wave workgroups per CU (grid-stride over
- *              the K x ceil(L / 1024) units).
+ *   "expand_waves" 1..256 (default 64): one-wave workgroups per CU of the expansion kernel
+ *              (flm_prg_expand[_dev]), each taking a contiguous run of the K x ceil(L / 1024)
+ *              seed-major (seed, 1024-slot chunk) units.
  *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev runs
  *              rounds as ONE small-round launch never | when rows and mask words are both
  *              <= 2^22 (BASELINE c2) | whenever the window allows it (mask_hi % 16 == 0 or

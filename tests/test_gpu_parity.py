@@ -72,19 +72,18 @@ def test_prg_expand_batch_vs_oracle(eng):
             assert np.array_equal(got[k], O.prg(seeds[k].tobytes(), L)), (k, L)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
-def test_prg_expand_dev_kernel_forms(eng, mode):
-    """prg_expand_kernel in every store form (expand_mode: bit 0 nontemporal, bit 1 LDS-staged) and
-    with a grid smaller than the unit count (grid-stride): ragged L (tails inside a 16-word block,
-    inside a 1024-slot chunk), PRG windows (slot0), a padded pitch that must stay untouched, and the
-    whole output against oracle.prg (SA_ServiceAgent.py:596-603)."""
+@pytest.mark.parametrize("waves", [1, 64, 256])
+def test_prg_expand_dev_kernel(eng, waves):
+    """prg_expand_kernel (flm_prg_expand_dev) with grids from far fewer workgroups than units (each
+    takes a run of units across several seeds) to more workgroups than units: ragged L (tails inside
+    a 16-word block, inside a 1024-slot chunk), PRG windows (slot0), a padded pitch that must stay
+    untouched, and the whole output against oracle.prg (SA_ServiceAgent.py:596-603)."""
     import torch
-    g = rng(40 + mode)
-    eng.set_tuning("expand_mode", mode)
+    g = rng(40 + waves)
+    eng.set_tuning("expand_waves", waves)
     try:
-        for L, slot0, pad, waves in ((1, 0, 4, 16), (17, 16, 0, 16), (1023, 4096, 8, 1), (1025, 0, 4, 2),
-                                     (5000, 2**20 - 5008, 12, 16), (40000, 2**30, 0, 32)):
-            eng.set_tuning("expand_waves", waves)
+        for L, slot0, pad in ((1, 0, 4), (17, 16, 0), (1023, 4096, 8), (1025, 0, 4), (5000, 2**20 - 5008, 12),
+                              (40000, 2**30, 0)):
             K = int(g.integers(1, 40))
             seeds = g.integers(0, 256, size=(K, 32), dtype=np.uint8)
             pitch = (L + 3) // 4 * 4 + pad
@@ -93,12 +92,11 @@ def test_prg_expand_dev_kernel_forms(eng, mode):
             torch.cuda.synchronize()
             got = out.cpu().numpy().view(np.uint32)
             for k in range(K):
-                assert np.array_equal(got[k, :L], O.prg(seeds[k].tobytes(), L, slot0)), (mode, L, slot0, k)
-            assert np.all(got[:, L:] == 0x3C3C3C3C), (mode, L, "wrote past L")
+                assert np.array_equal(got[k, :L], O.prg(seeds[k].tobytes(), L, slot0)), (waves, L, slot0, k)
+            assert np.all(got[:, L:] == 0x3C3C3C3C), (waves, L, "wrote past L")
             assert eng.last_plan()["variant"] == 101
     finally:
-        eng.set_tuning("expand_mode", 0)
-        eng.set_tuning("expand_waves", 16)
+        eng.set_tuning("expand_waves", 64)
 
 
 def test_keystream_golden(eng, golden):

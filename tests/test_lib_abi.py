@@ -78,4 +78,4 @@ def test_round6_entry_points_reject_null_handles(lib):
     v = ctypes.c_int(7)
     assert lib.flm_get_tuning(None, b"pairing", ctypes.byref(v)) == -1 and b"NULL" in lib.flm_last_error(None)
     assert v.value == 7
-    assert lib.flm_set_tuning(None, b"expand_mode", 1) == -1
+    assert lib.flm_set_tuning(None, b"expand_waves", 8) == -1

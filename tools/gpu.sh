@@ -123,6 +123,14 @@ for step in "$@"; do
       timeout -k 10 300 python -u tools/probes/expand_probe.py > "$O/${TAG}_expand_probe.log" 2>&1 \
         || { tail -30 "$O/${TAG}_expand_probe.log"; exit 1; }
       cat "$O/${TAG}_expand_probe.log" | grep -v amdgpu.ids ;;
+    stallevict)
+      # KFD's per-process queue-eviction counter (sysfs evicted_ms) around every server unmask of the
+      # c5 agent run (tools/probes/evict_probe_run.py), 3 runs x 3 iterations
+      for v in 1 2 3; do
+        timeout -k 10 300 python -u tools/probes/evict_probe_run.py -c flamingo -n 4096 --vector_len 1048576 -i 3 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_evict_$v.log" 2>&1 || { tail -30 "$O/${TAG}_evict_$v.log"; exit 1; }
+        echo "== run $v"; grep -h "evict_probe" "$O/${TAG}_evict_$v.log" | cut -c1-400
+      done ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \

@@ -19,3 +19,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 # standalone mask expansion (flm_prg_expand_dev, c5's D seeds x 2^20): kernel trace + stats, then its write traffic
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_expand -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_${TAG}_expand_pmc -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand_pmc.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_SALU --output-format csv -d $R/gpurun_out/prof_${TAG}_expand_pmc3 -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand_pmc3.log 2>&1 || exit $?

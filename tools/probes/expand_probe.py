@@ -1,5 +1,5 @@
-"""A/B of the expansion kernel (flm_prg_expand_dev, prg_expand_kernel): store form (expand_mode 0..3:
-bit 0 nontemporal, bit 1 LDS-staged) x one-wave workgroups per CU (expand_waves), at the bench's
+"""A/B of the expansion kernel (flm_prg_expand_dev, prg_expand_kernel): one-wave workgroups per CU
+(expand_waves; round 6's first pass also swept the store form, profiles/r06_expand_probe.log), at the bench's
 shape (K = 962 pair seeds x L = 2^20), median of 7 launches each, rounds interleaved so the clock
 drifts alike; every configuration's output is checked against oracle.prg on windows (checker only).
 Also times the summing kernel's mask-only launch of the same seeds (the same-run ChaCha ceiling)."""
@@ -47,7 +47,7 @@ def check():
 
 
 acc = torch.empty(L, dtype=torch.int32, device=dev)
-configs = [(m, w) for m in (0, 1, 2, 3) for w in (8, 16, 32)]
+configs = [(0, w) for w in (32, 64, 96, 128, 256)]
 res = {c: [] for c in configs}
 ceil = []
 with torch.cuda.stream(s):
@@ -55,7 +55,6 @@ with torch.cuda.stream(s):
         eng.seed_table_dev(d_seeds, d_signs, stream=s)
         ceil.append(timed(lambda: eng.aggregate_dev(None, K, acc, L=L, stream=s)))
         for m, w in configs:
-            eng.set_tuning("expand_mode", m)
             eng.set_tuning("expand_waves", w)
             out.fill_(0x3C3C3C3C)
             ms = timed(lambda: eng.prg_expand_dev(d_seeds, out, L, stream=s))
@@ -68,5 +67,5 @@ c = float(np.median(ceil))
 print(f"mask-only summing launch (same seeds, K={K}): {c:.4f} ms = {words / c / 1e6:.1f} G words/s", flush=True)
 for (m, w), v in sorted(res.items(), key=lambda kv: np.median(kv[1])):
     ms = float(np.median(v))
-    print(f"mode {m} (nt {m & 1}, lds {m >> 1 & 1}) waves/CU {w:2d}: {ms:.4f} ms  {4 * words / ms / 1e6:7.1f} GB/s written"
+    print(f"waves/CU {w:2d}: {ms:.4f} ms  {4 * words / ms / 1e6:7.1f} GB/s written"
           f"  {words / ms / 1e6:6.1f} G words/s = {c / ms:.3f} of the ceiling   runs {[round(x, 4) for x in v]}", flush=True)
