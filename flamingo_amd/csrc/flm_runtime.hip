@@ -173,9 +173,9 @@ struct flm_ctx {
     int tune_small = 1;      // one-launch small_round_kernel: 0 never, 1 small rounds (auto), 2 whenever legal
     int tune_pairing = 1;    // rows/masks on different tiles: 0 interleaved items, 1 dual-tile items (measured 1.97 vs 3.46 ms),
                              // 2 same-tile window items (plan_window_same; 0.228 vs 0.188 ms at G = 8, r02_ab_window_same.log)
-    int tune_expand_waves = 64;  // prg_expand_kernel one-wave workgroups per CU: 16 / 32 / 64 -> 1.57 / 1.43 / 1.38 ms
-                                 // at K = 962, L = 2^20 (profiles/r06_expand_probe_waves.log); ~9 fit a SIMD at once,
-                                 // the rest queue behind them and even out the runs' ends
+    int tune_expand_waves = 128;  // prg_expand_kernel one-wave workgroups per CU: 16 / 32 / 64 / 128 -> 1.57 / 1.43 /
+                                  // 1.37 / 1.34 ms at K = 962, L = 2^20 (profiles/r06_expand_probe_waves*.log); ~9 fit
+                                  // a SIMD at once, the rest queue behind them and even out the runs' ends
     int n_cus = 0;               // the device's CU count (flm_init)
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };

@@ -186,7 +186,7 @@ int flm_last_plan(const flm_ctx *ctx, int *items, int *tile_slots, int *atomics,
  *              runs cooperatively.
  *   "ec_spread" 0 (default) .. 64: KiB of LDS reserved per 64-lane workgroup of the
  *              per-lane combine kernels (caps their workgroups per CU).
- *   "expand_waves" 1..256 (default 64): one-wave workgroups per CU of the expansion kernel
+ *   "expand_waves" 1..256 (default 128): one-wave workgroups per CU of the expansion kernel
  *              (flm_prg_expand[_dev]), each taking a contiguous run of the K x ceil(L / 1024)
  *              seed-major (seed, 1024-slot chunk) units.
  *   "small"   0 | 1 (default) | 2: flm_aggregate_unmask_dev runs

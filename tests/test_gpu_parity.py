@@ -96,7 +96,7 @@ def test_prg_expand_dev_kernel(eng, waves):
             assert np.all(got[:, L:] == 0x3C3C3C3C), (waves, L, "wrote past L")
             assert eng.last_plan()["variant"] == 101
     finally:
-        eng.set_tuning("expand_waves", 64)
+        eng.set_tuning("expand_waves", 128)
 
 
 def test_keystream_golden(eng, golden):

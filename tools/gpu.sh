@@ -126,6 +126,7 @@ for step in "$@"; do
     stallevict)
       # KFD's per-process queue-eviction counter (sysfs evicted_ms) around every server unmask of the
       # c5 agent run (tools/probes/evict_probe_run.py), 3 runs x 3 iterations
+      ls /sys/class/kfd/kfd 2>&1 | head; ls /sys/class/kfd/kfd/proc 2>&1 | head
       for v in 1 2 3; do
         timeout -k 10 300 python -u tools/probes/evict_probe_run.py -c flamingo -n 4096 --vector_len 1048576 -i 3 \
           --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_evict_$v.log" 2>&1 || { tail -30 "$O/${TAG}_evict_$v.log"; exit 1; }

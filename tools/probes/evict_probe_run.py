@@ -18,13 +18,16 @@ PID = os.getpid()
 
 
 def evicted():
+    """evicted_ms of every KFD process directory visible (sysfs names them by the HOST pid, which a
+    container's getpid() does not give: on the box this process is the only GPU user)."""
     out = {}
-    for f in sorted(glob.glob(f"/sys/class/kfd/kfd/proc/{PID}/stats_*/evicted_ms")):
+    for f in sorted(glob.glob("/sys/class/kfd/kfd/proc/*/stats_*/evicted_ms")):
+        key = f.split("/")[-3] + "/" + f.split("/")[-2]
         try:
             with open(f) as fh:
-                out[f.split("/")[-2]] = int(fh.read().strip() or 0)
+                out[key] = int(fh.read().strip() or 0)
         except OSError as e:
-            out[f.split("/")[-2]] = f"error {e}"
+            out[key] = f"error {e}"
     return out
 
 
@@ -53,12 +56,12 @@ def unmask(self, seeds, signs):
 
 
 ingest.VectorStore.unmask = unmask
-print(f"[evict_probe] pid {PID}; kfd proc dir: {os.path.isdir(f'/sys/class/kfd/kfd/proc/{PID}')}; "
+print(f"[evict_probe] pid {PID}; kfd proc dirs: {glob.glob('/sys/class/kfd/kfd/proc/*')}; "
       f"start {evicted()}", flush=True)
 sys.argv = ["flamingo_amd.abides"] + sys.argv[1:]
 try:
     runpy.run_module("flamingo_amd.abides", run_name="__main__", alter_sys=True)
 finally:
-    print(f"[evict_probe] end {evicted()}; stats files "
-          f"{sorted(os.listdir(f'/sys/class/kfd/kfd/proc/{PID}')) if os.path.isdir(f'/sys/class/kfd/kfd/proc/{PID}') else None}",
-          flush=True)
+    dirs = glob.glob("/sys/class/kfd/kfd/proc/*")
+    print(f"[evict_probe] end {evicted()}; kfd proc dirs {dirs}; files of the first "
+          f"{sorted(os.listdir(dirs[0])) if dirs else None}", flush=True)
