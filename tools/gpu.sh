@@ -132,6 +132,18 @@ for step in "$@"; do
           --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_evict_$v.log" 2>&1 || { tail -30 "$O/${TAG}_evict_$v.log"; exit 1; }
         echo "== run $v"; grep -h "evict_probe" "$O/${TAG}_evict_$v.log" | cut -c1-400
       done ;;
+    stallthp)
+      # the eviction counter with transparent huge pages off for the process (PR_SET_THP_DISABLE) vs on,
+      # alternating, 3 iterations each; then /proc/vmstat's THP / compaction / migration counters
+      grep -h "thp_\|compact_\|pgmigrate" /proc/vmstat > "$O/${TAG}_vmstat_before.txt" 2>/dev/null
+      for v in off on off on off off; do
+        if [ $v = off ]; then fl="--thp-off"; else fl=""; fi
+        timeout -k 10 300 python -u tools/probes/evict_probe_run.py $fl -c flamingo -n 4096 --vector_len 1048576 -i 3 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_thp_$v.log" 2>&1 || { tail -30 "$O/${TAG}_thp_$v.log"; exit 1; }
+        echo "== thp $v"; grep -h "evict_probe\] unmask" "$O/${TAG}_thp_$v.log" | cut -c1-60
+        cat "$O/${TAG}_thp_$v.log" >> "$O/${TAG}_thp_all.txt"
+      done
+      grep -h "thp_\|compact_\|pgmigrate" /proc/vmstat > "$O/${TAG}_vmstat_after.txt" 2>/dev/null; true ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \

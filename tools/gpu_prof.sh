@@ -20,3 +20,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_expand -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/prof_${TAG}_expand_pmc -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand_pmc.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_INSTS_SALU --output-format csv -d $R/gpurun_out/prof_${TAG}_expand_pmc3 -o run -- python3 $R/tools/expand_bench.py > $R/gpurun_out/prof_${TAG}_expand_pmc3.log 2>&1 || exit $?
+cd $R && python3 tools/summarize_profile.py gpurun_out/prof_${TAG}_expand_summary.json gpurun_out/prof_${TAG}_expand gpurun_out/prof_${TAG}_expand_pmc gpurun_out/prof_${TAG}_expand_pmc3 > /dev/null

@@ -15,6 +15,12 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 PID = os.getpid()
+if "--thp-off" in sys.argv:  # transparent huge pages off for this process (prctl PR_SET_THP_DISABLE), first thing
+    import ctypes
+    sys.argv.remove("--thp-off")
+    if ctypes.CDLL(None, use_errno=True).prctl(41, 1, 0, 0, 0) != 0:
+        sys.exit(f"evict_probe_run: prctl(PR_SET_THP_DISABLE) failed, errno {ctypes.get_errno()}")
+    print("[evict_probe] THP disabled for this process", flush=True)
 
 
 def evicted():
