@@ -317,6 +317,10 @@ struct flm_group {
         size_t dirty = 0;  // partial words [0, dirty) may hold an earlier round's data
     };
     std::vector<Rank> rk;
+    // pinned landing buffer of flm_group_aggregate_unmask's shards: the caller's `out` is pageable, and
+    // a HIP copy into pageable memory pins it for the driver (flm_runtime.hip HostCopies: DESIGN.md 6)
+    uint32_t *hout = nullptr;
+    size_t hout_cap = 0;
     std::string err;
 };
 
@@ -497,6 +501,7 @@ void flm_group_free(flm_group *g) {
         if (g->rk[r].xdone) (void)hipEventDestroy(g->rk[r].xdone);
         flm_free(g->ctx[r]);
     }
+    if (g->hout) (void)hipHostFree(g->hout);
     delete g;
 }
 
@@ -546,6 +551,14 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         if ((rc_ = wait_previous_exchange(g, r))) return rc_;
     for (int r = 0; X && r < G; ++r)
         if ((rc_ = clear_stale_tail(g, r, L))) return rc_;
+    if (g->hout_cap < L) {  // the last call synchronised every rank: nothing reads the old buffer
+        if (g->hout) (void)hipHostFree(g->hout);
+        g->hout = nullptr;
+        g->hout_cap = 0;
+        if (hipHostMalloc(&g->hout, L * sizeof(uint32_t), hipHostMallocPortable) != hipSuccess)
+            return gfail(g, FLM_ENOMEM, "group: pinned output buffer");
+        g->hout_cap = L;
+    }
     std::vector<int> rcs(G, 0);
     auto work = [&](int r) {
         int c0, c1;
@@ -574,11 +587,13 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         flm_shard_bounds(L, G, r, &lo, &hi, nullptr);
         if (hi <= lo) continue;
         (void)hipSetDevice(g->dev[r]);
-        hipError_t e = hipMemcpyAsync(out + lo, g->rk[r].shard, (hi - lo) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                      flm::rt::stream_of(g->ctx[r]));
+        hipError_t e = hipMemcpyAsync(g->hout + lo, g->rk[r].shard, (hi - lo) * sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, flm::rt::stream_of(g->ctx[r]));
         if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("shard D2H: ") + hipGetErrorString(e));
     }
-    return flm_group_sync(g);
+    if (int rc = flm_group_sync(g)) return rc;
+    std::memcpy(out, g->hout, L * sizeof(uint32_t));
+    return 0;
 }
 
 // Device-resident form: rank r's rows are already in its HBM (d_rows[r], n_rows[r] rows at

@@ -177,6 +177,8 @@ struct flm_ctx {
                                   // 1.37 / 1.34 ms at K = 962, L = 2^20 (profiles/r06_expand_probe_waves*.log); ~9 fit
                                   // a SIMD at once, the rest queue behind them and even out the runs' ends
     int n_cus = 0;               // the device's CU count (flm_init)
+    void *bounce = nullptr;      // pinned bounce buffer of the host-pointer entry points (HostCopies)
+    size_t bounce_cap = 0;
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
 
@@ -901,7 +903,8 @@ bool host_pinned(const void *p) {
 // rows are packed into a pinned staging ring (kStageBytes per buffer, two
 // buffers) so the copy engine sees few large transfers while the CPU fills
 // the other buffer.  The VECTOR bodies of the reference are pageable numpy
-// arrays (SA_ServiceAgent.py:210).
+// arrays (SA_ServiceAgent.py:210).  No pageable row is ever handed to a HIP copy
+// (HostCopies below says why).
 constexpr size_t kStageBytes = 32u << 20;
 
 int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint64_t pitch) {
@@ -947,11 +950,6 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
         }
     }
     if (pageable.empty()) return 0;
-    if (slot_bytes > kStageBytes) {  // very long rows: one DMA per row through HIP's own staging
-        for (int i : pageable)
-            FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)i * pitch, rows[i], row_bytes, hipMemcpyHostToDevice, ctx->stream));
-        return 0;
-    }
     if (ctx->stage_cap < kStageBytes) {
         for (int b = 0; b < 2; ++b) {
             if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
@@ -961,10 +959,24 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
         }
         ctx->stage_cap = kStageBytes;
     }
-    const size_t per_buf = kStageBytes / slot_bytes;  // rows per staging buffer
     size_t k = 0;
     int b = 0;
     bool used[2] = {false, false};
+    if (slot_bytes > kStageBytes) {  // very long rows: each in kStageBytes pieces through the same ring
+        for (int i : pageable)
+            for (size_t off = 0; off < row_bytes; off += kStageBytes) {
+                const size_t n = std::min(kStageBytes, row_bytes - off);
+                if (used[b]) FLM_HIP(ctx, hipEventSynchronize(ctx->stage_done[b]));
+                std::memcpy(ctx->stage[b], reinterpret_cast<const uint8_t *>(rows[i]) + off, n);
+                FLM_HIP(ctx, hipMemcpyAsync(reinterpret_cast<uint8_t *>(dst + (size_t)i * pitch) + off, ctx->stage[b], n,
+                                            hipMemcpyHostToDevice, ctx->stream));
+                FLM_HIP(ctx, hipEventRecord(ctx->stage_done[b], ctx->stream));
+                used[b] = true;
+                b ^= 1;
+            }
+        return 0;
+    }
+    const size_t per_buf = kStageBytes / slot_bytes;  // rows per staging buffer
     while (k < pageable.size()) {
         if (used[b]) FLM_HIP(ctx, hipEventSynchronize(ctx->stage_done[b]));  // DMA out of this buffer done
         uint8_t *st = static_cast<uint8_t *>(ctx->stage[b]);
@@ -985,12 +997,99 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
     return 0;
 }
 
-int upload_seeds(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs, int K) {
+// The host-pointer entry points move the caller's arrays through the context's pinned bounce
+// buffer (ctx->bounce), never straight between a HIP copy and the caller's pageable pages.  For a
+// large pageable copy the HIP runtime pins those pages for the DMA (a KFD userptr allocation; its log:
+// "HSA Copy Using Pinned resource"); when the process later unmaps them (a numpy array freed), the
+// driver evicts ALL of the process's GPU queues while it revalidates: 20-40 ms in which nothing of
+// ours runs.  That was the agent run's unmask stall (the driver's per-process
+// evicted_ms grows by exactly the stall, and the stalls go away when the runtime never pins,
+// GPU_PINNED_MIN_XFER_SIZE).  One bounce buffer per context: these calls are synchronous (or, for a
+// group's ranks, synchronised before the call returns), so a call reuses it only after the last
+// call's copies out of it have completed; reserve() sizes it for the whole call before its first copy.
+class HostCopies {
+  public:
+    HostCopies(flm_ctx *ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
+    static size_t room(size_t n) { return round_up(n, 256); }
+    int reserve(size_t bytes) {  // the sum of room(n) over the call's copies
+        if (bytes > ctx_->bounce_cap) {
+            if (ctx_->bounce) (void)hipHostFree(ctx_->bounce);  // waits for the device: nothing reads it after
+            ctx_->bounce = nullptr;
+            ctx_->bounce_cap = 0;
+            const size_t want = flm::rt::grow_bytes(bytes);
+            const hipError_t e = hipHostMalloc(&ctx_->bounce, want, hipHostMallocDefault);
+            if (e != hipSuccess) return fail(ctx_, FLM_ENOMEM, "pinned bounce buffer of %zu bytes: %s", want, hipGetErrorString(e));
+            ctx_->bounce_cap = want;
+        }
+        cap_ = bytes;
+        return 0;
+    }
+    // d_dst <- h_src (n bytes): copied into the bounce buffer now, DMA enqueued on the stream
+    int in(void *d_dst, const void *h_src, size_t n) {
+        if (!n) return 0;
+        uint8_t *b = take(n);
+        if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", n, cap_);
+        std::memcpy(b, h_src, n);
+        FLM_HIP(ctx_, hipMemcpyAsync(d_dst, b, n, hipMemcpyHostToDevice, s_));
+        return 0;
+    }
+    // rows x width bytes, host rows at h_pitch, device rows at d_pitch
+    int in2d(void *d_dst, size_t d_pitch, const void *h_src, size_t h_pitch, size_t width, size_t rows) {
+        if (!width || !rows) return 0;
+        uint8_t *b = take(width * rows);
+        if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
+        for (size_t r = 0; r < rows; ++r) std::memcpy(b + r * width, static_cast<const uint8_t *>(h_src) + r * h_pitch, width);
+        FLM_HIP(ctx_, hipMemcpy2DAsync(d_dst, d_pitch, b, width, width, rows, hipMemcpyHostToDevice, s_));
+        return 0;
+    }
+    // h_dst <- d_src: DMA into the bounce buffer now, handed to the caller by finish()
+    int out(void *h_dst, const void *d_src, size_t n) { return out2d(h_dst, n, d_src, n, n, 1); }
+    int out2d(void *h_dst, size_t h_pitch, const void *d_src, size_t d_pitch, size_t width, size_t rows) {
+        if (!width || !rows) return 0;
+        uint8_t *b = take(width * rows);
+        if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
+        FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(b, d_src, width, hipMemcpyDeviceToHost, s_)
+                                : hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
+        outs_.push_back({h_dst, h_pitch, b, width, rows});
+        return 0;
+    }
+    // wait for the stream, then copy the outputs to the caller
+    int finish() {
+        FLM_HIP(ctx_, hipStreamSynchronize(s_));
+        for (const Out &o : outs_)
+            for (size_t r = 0; r < o.rows; ++r)
+                std::memcpy(static_cast<uint8_t *>(o.dst) + r * o.pitch, o.src + r * o.width, o.width);
+        outs_.clear();
+        return 0;
+    }
+
+  private:
+    struct Out {
+        void *dst;
+        size_t pitch;
+        const uint8_t *src;
+        size_t width, rows;
+    };
+    uint8_t *take(size_t n) {
+        if (off_ + room(n) > cap_) return nullptr;
+        uint8_t *b = static_cast<uint8_t *>(ctx_->bounce) + off_;
+        off_ += room(n);
+        return b;
+    }
+    flm_ctx *ctx_;
+    hipStream_t s_;
+    size_t cap_ = 0, off_ = 0;
+    std::vector<Out> outs_;
+};
+
+size_t seeds_room(int K) { return K > 0 ? HostCopies::room((size_t)K * 32) + HostCopies::room((size_t)K) : 0; }
+
+int upload_seeds(flm_ctx *ctx, HostCopies &hc, const uint8_t *seeds, const int8_t *signs, int K) {
     FLM_HIP(ctx, ctx->seeds.reserve(std::max<size_t>(1, (size_t)K) * 32));
     FLM_HIP(ctx, ctx->signs.reserve(std::max<size_t>(1, (size_t)K)));
     if (K > 0) {
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->seeds.p, seeds, (size_t)K * 32, hipMemcpyHostToDevice, ctx->stream));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->signs.p, signs, (size_t)K, hipMemcpyHostToDevice, ctx->stream));
+        if (int rc = hc.in(ctx->seeds.p, seeds, (size_t)K * 32)) return rc;
+        if (int rc = hc.in(ctx->signs.p, signs, (size_t)K)) return rc;
     }
     return 0;
 }
@@ -1105,10 +1204,13 @@ int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uin
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
-    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    HostCopies hc(ctx, ctx->stream);  // the group synchronises every rank before its call returns
+    if (int rc = hc.reserve(seeds_room(K))) return rc;
+    if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
     return flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, N, ctx->seeds.as<uint8_t>(),
                                     ctx->signs.as<int8_t>(), K, L, mask_lo, mask_hi, 0, d_out, ctx->stream);
 }
+
 }  // namespace rt
 }  // namespace flm
 
@@ -1172,6 +1274,7 @@ void flm_free(flm_ctx *ctx) {
         (void)hipEventDestroy(s->done);
         delete s;
     }
+    if (ctx->bounce) (void)hipHostFree(ctx->bounce);
     for (int i = 0; i < 2; ++i) {
         if (ctx->stage[i]) (void)hipHostFree(ctx->stage[i]);
         if (ctx->stage_done[i]) (void)hipEventDestroy(ctx->stage_done[i]);
@@ -1204,14 +1307,15 @@ int flm_aggregate_unmask(flm_ctx *ctx, const uint32_t *const *rows, int N, const
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     if (int rc = upload_rows(ctx, rows, N, L, pitch)) return rc;
-    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    HostCopies hc(ctx, ctx->stream);
+    if (int rc = hc.reserve(seeds_room(K) + HostCopies::room(L * sizeof(uint32_t)))) return rc;
+    if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
     FLM_HIP(ctx, ctx->out.reserve(L * sizeof(uint32_t)));
     if (int rc = flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, N, ctx->seeds.as<uint8_t>(),
                                           ctx->signs.as<int8_t>(), K, L, 0, L, 0, ctx->out.as<uint32_t>(), ctx->stream))
         return rc;
-    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->out.p, L * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    if (int rc = hc.out(out, ctx->out.p, L * sizeof(uint32_t))) return rc;
+    return hc.finish();
 }
 
 static int check_aggregate_args(flm_ctx *ctx, const uint32_t *d_rows, size_t row_pitch, int N, int K, size_t L,
@@ -1302,22 +1406,22 @@ int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, 
     if (int rc = check_range(ctx, L)) return rc;
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
+    const size_t plane = (size_t)N * L * 4;
+    HostCopies hc(ctx, ctx->stream);
+    if (int rc = hc.reserve((x ? HostCopies::room(plane) : 0) + seeds_room((int)K) + HostCopies::room(plane))) return rc;
     uint32_t *d_x = nullptr;
     if (x) {
         FLM_HIP(ctx, ctx->rows.reserve((size_t)N * pitch * sizeof(uint32_t)));
-        FLM_HIP(ctx, hipMemcpy2DAsync(ctx->rows.p, pitch * 4, x, L * 4, L * 4, (size_t)N, hipMemcpyHostToDevice,
-                                      ctx->stream));
+        if (int rc = hc.in2d(ctx->rows.p, pitch * 4, x, L * 4, L * 4, (size_t)N)) return rc;
         d_x = ctx->rows.as<uint32_t>();
     }
-    if (int rc = upload_seeds(ctx, seeds, signs, (int)K)) return rc;
+    if (int rc = upload_seeds(ctx, hc, seeds, signs, (int)K)) return rc;
     FLM_HIP(ctx, ctx->out.reserve((size_t)N * pitch * sizeof(uint32_t)));
     if (int rc = flm_client_mask_dev(ctx, d_x, pitch, N, seg, ctx->seeds.as<uint8_t>(), signs, L, ctx->out.as<uint32_t>(),
                                      ctx->stream))
         return rc;
-    FLM_HIP(ctx, hipMemcpy2DAsync(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)N, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    if (int rc = hc.out2d(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)N)) return rc;
+    return hc.finish();
 }
 
 int flm_client_mask_dev(flm_ctx *ctx, const uint32_t *d_x, size_t pitch, int N, const int64_t *seg,
@@ -1373,16 +1477,16 @@ int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t
     if (int rc = check_range(ctx, slot0 + L)) return rc;
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
+    HostCopies hc(ctx, ctx->stream);
+    if (int rc = hc.reserve(HostCopies::room((size_t)K * 32) + HostCopies::room((size_t)K * L * 4))) return rc;
     FLM_HIP(ctx, ctx->seeds.reserve((size_t)K * 32));
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->seeds.p, seeds, (size_t)K * 32, hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = hc.in(ctx->seeds.p, seeds, (size_t)K * 32)) return rc;
     FLM_HIP(ctx, ctx->out.reserve((size_t)K * pitch * sizeof(uint32_t)));
     if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, ctx->out.as<uint32_t>(), pitch,
                                     ctx->stream))
         return rc;
-    FLM_HIP(ctx, hipMemcpy2DAsync(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)K, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    if (int rc = hc.out2d(out, L * 4, ctx->out.p, pitch * 4, L * 4, (size_t)K)) return rc;
+    return hc.finish();
 }
 
 int flm_prg_expand_dev(flm_ctx *ctx, const uint8_t *d_seeds, int K, size_t L, uint64_t slot0, uint32_t *d_out,
@@ -1435,17 +1539,18 @@ int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs,
     if (int rc = check_range(ctx, slot0 + L)) return rc;
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
+    HostCopies hc(ctx, ctx->stream);
+    if (int rc = hc.reserve(2 * HostCopies::room(L * 4) + seeds_room(K))) return rc;
     FLM_HIP(ctx, ctx->rows.reserve(pitch * sizeof(uint32_t)));
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->rows.p, acc, L * 4, hipMemcpyHostToDevice, ctx->stream));
-    if (int rc = upload_seeds(ctx, seeds, signs, K)) return rc;
+    if (int rc = hc.in(ctx->rows.p, acc, L * 4)) return rc;
+    if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
     FLM_HIP(ctx, ctx->out.reserve(pitch * sizeof(uint32_t)));
     if (int rc = flm_aggregate_unmask_dev(ctx, ctx->rows.as<uint32_t>(), pitch, 1, ctx->seeds.as<uint8_t>(),
                                           ctx->signs.as<int8_t>(), K, L, 0, L, slot0, ctx->out.as<uint32_t>(),
                                           ctx->stream))
         return rc;
-    FLM_HIP(ctx, hipMemcpyAsync(acc, ctx->out.p, L * 4, hipMemcpyDeviceToHost, ctx->stream));
-    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    if (int rc = hc.out(acc, ctx->out.p, L * 4)) return rc;
+    return hc.finish();
 }
 
 int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8], uint64_t counter, const uint8_t *in,
@@ -1463,12 +1568,13 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
                 ((uint32_t)nonce[4 * i + 3] << 24);
     FLM_HIP(ctx, ctx->bytes_in.reserve(n));
     FLM_HIP(ctx, ctx->bytes_out.reserve(n));
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->bytes_in.p, in, n, hipMemcpyHostToDevice, ctx->stream));
+    HostCopies hc(ctx, ctx->stream);
+    if (int rc = hc.reserve(2 * HostCopies::room(n))) return rc;
+    if (int rc = hc.in(ctx->bytes_in.p, in, n)) return rc;
     FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, ctx->bytes_in.as<uint8_t>(), ctx->bytes_out.as<uint8_t>(), n,
                                           ctx->stream));
-    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->bytes_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
-    FLM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    if (int rc = hc.out(out, ctx->bytes_out.p, n)) return rc;
+    return hc.finish();
 }
 
 int flm_plan_aggregate(int subtiles, int pairing, size_t row_pitch, int N, int K, size_t L, size_t mask_lo,
@@ -1639,20 +1745,28 @@ int flm_ec_combine(flm_ctx *ctx, const uint8_t *c1, const uint8_t *shares, const
     FLM_HIP(ctx, ctx->ec_dig.reserve((size_t)D * 32));
     FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)D * 4));
     hipStream_t s = ctx->stream;
+    HostCopies hc(ctx, s);
+    using HC = HostCopies;
+    if (int rc = hc.reserve(HC::room(nsh) + HC::room((size_t)T * 32) + HC::room((size_t)D * 64) + HC::room((size_t)D * 4) +
+                            HC::room((size_t)D * 64) + HC::room((size_t)D * 32)))
+        return rc;
     if (T > 0) {
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, shares, nsh, hipMemcpyHostToDevice, s));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lambdas, (size_t)T * 32, hipMemcpyHostToDevice, s));
+        if (int rc = hc.in(ctx->ec_in.p, shares, nsh)) return rc;
+        if (int rc = hc.in(ctx->ec_scal.p, lambdas, (size_t)T * 32)) return rc;
     }
-    if (c1) FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_base.p, c1, (size_t)D * 64, hipMemcpyHostToDevice, s));
+    if (c1)
+        if (int rc = hc.in(ctx->ec_base.p, c1, (size_t)D * 64)) return rc;
     if (int rc = flm_ec_combine_dev(ctx, c1 ? ctx->ec_base.as<uint8_t>() : nullptr, ctx->ec_in.as<uint8_t>(),
                                     ctx->ec_scal.as<uint8_t>(), T, D, negate, ctx->ec_out.as<uint8_t>(),
                                     ctx->ec_dig.as<uint8_t>(), ctx->ec_flags.as<uint32_t>(), s))
         return rc;
     std::vector<uint32_t> fl(D);
-    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)D * 4, hipMemcpyDeviceToHost, s));
-    if (points_out) FLM_HIP(ctx, hipMemcpyAsync(points_out, ctx->ec_out.p, (size_t)D * 64, hipMemcpyDeviceToHost, s));
-    if (seeds_out) FLM_HIP(ctx, hipMemcpyAsync(seeds_out, ctx->ec_dig.p, (size_t)D * 32, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (int rc = hc.out(fl.data(), ctx->ec_flags.p, (size_t)D * 4)) return rc;
+    if (points_out)
+        if (int rc = hc.out(points_out, ctx->ec_out.p, (size_t)D * 64)) return rc;
+    if (seeds_out)
+        if (int rc = hc.out(seeds_out, ctx->ec_dig.p, (size_t)D * 32)) return rc;
+    if (int rc = hc.finish()) return rc;
     if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
     for (int i = 0; i < D; ++i)
         if (fl[i] & 3u)
@@ -1719,15 +1833,18 @@ int flm_shamir_combine(flm_ctx *ctx, const uint8_t *shares, const uint8_t *lambd
     FLM_HIP(ctx, ctx->ec_in.reserve((size_t)std::max(T, 1) * M * 32));
     FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)std::max(T, 1) * 32));
     FLM_HIP(ctx, ctx->ec_dig.reserve((size_t)M * 32));
+    HostCopies hc(ctx, s);
+    if (int rc = hc.reserve(HostCopies::room((size_t)T * M * 32) + HostCopies::room((size_t)T * 32) +
+                            HostCopies::room((size_t)M * 32)))
+        return rc;
     if (T > 0) {
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, shares, (size_t)T * M * 32, hipMemcpyHostToDevice, s));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lambdas, (size_t)T * 32, hipMemcpyHostToDevice, s));
+        if (int rc = hc.in(ctx->ec_in.p, shares, (size_t)T * M * 32)) return rc;
+        if (int rc = hc.in(ctx->ec_scal.p, lambdas, (size_t)T * 32)) return rc;
     }
     FLM_HIP(ctx, flm::launch_shamir_combine(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), T, M,
                                             ctx->ec_dig.as<uint8_t>(), s));
-    FLM_HIP(ctx, hipMemcpyAsync(seeds_out, ctx->ec_dig.p, (size_t)M * 32, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipStreamSynchronize(s));
-    return 0;
+    if (int rc = hc.out(seeds_out, ctx->ec_dig.p, (size_t)M * 32)) return rc;
+    return hc.finish();
 }
 
 int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int n, uint8_t *out, uint32_t *flags_out) {
@@ -1742,8 +1859,12 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     FLM_HIP(ctx, ctx->ec_out.reserve((size_t)n * 64));
     FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)n * 4));
     hipStream_t s = ctx->stream;
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, points, (size_t)n * 64, hipMemcpyHostToDevice, s));
-    FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, scalars, (size_t)n * 32, hipMemcpyHostToDevice, s));
+    HostCopies hc(ctx, s);
+    if (int rc = hc.reserve(2 * HostCopies::room((size_t)n * 64) + HostCopies::room((size_t)n * 32) +
+                            HostCopies::room((size_t)n * 4)))
+        return rc;
+    if (int rc = hc.in(ctx->ec_in.p, points, (size_t)n * 64)) return rc;
+    if (int rc = hc.in(ctx->ec_scal.p, scalars, (size_t)n * 32)) return rc;
     FLM_HIP(ctx, hipMemsetAsync(ctx->ec_flags.p, 0, (size_t)n * 4, s));
     FLM_HIP(ctx, flm::launch_ec_mul(ctx->ec_in.as<uint8_t>(), ctx->ec_scal.as<uint8_t>(), 1, 1, n,
                                     ctx->ec_jac.as<uint32_t>(), ctx->ec_flags.as<uint32_t>(), s,
@@ -1751,9 +1872,9 @@ int flm_ec_mul(flm_ctx *ctx, const uint8_t *points, const uint8_t *scalars, int 
     FLM_HIP(ctx, flm::launch_ec_finish(nullptr, ctx->ec_jac.as<uint32_t>(), 1, n, 0, ctx->ec_out.as<uint8_t>(),
                                        nullptr, ctx->ec_flags.as<uint32_t>(), s));
     std::vector<uint32_t> fl(n);
-    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->ec_out.p, (size_t)n * 64, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (int rc = hc.out(fl.data(), ctx->ec_flags.p, (size_t)n * 4)) return rc;
+    if (int rc = hc.out(out, ctx->ec_out.p, (size_t)n * 64)) return rc;
+    if (int rc = hc.finish()) return rc;
     if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
     for (int i = 0; i < n; ++i)
         if (fl[i] & 2u) return fail(ctx, FLM_EINVAL, "element %d: input is not a point on P-256", i);
@@ -1766,19 +1887,21 @@ static int h2c_run(flm_ctx *ctx, const uint8_t *msgs, const uint32_t *lens, uint
     hipStream_t s = ctx->stream;
     FLM_HIP(ctx, ctx->ec_out.reserve((size_t)n * 64));
     FLM_HIP(ctx, ctx->ec_flags.reserve((size_t)n * 4));
+    HostCopies hc(ctx, s);
+    if (int rc = hc.reserve(2 * HostCopies::room((size_t)n * 64) + 2 * HostCopies::room((size_t)n * 4))) return rc;
     if (msgs) {
         FLM_HIP(ctx, ctx->ec_in.reserve((size_t)n * 64));
         FLM_HIP(ctx, ctx->ec_scal.reserve((size_t)n * 4));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_in.p, msgs, (size_t)n * 64, hipMemcpyHostToDevice, s));
-        FLM_HIP(ctx, hipMemcpyAsync(ctx->ec_scal.p, lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        if (int rc = hc.in(ctx->ec_in.p, msgs, (size_t)n * 64)) return rc;
+        if (int rc = hc.in(ctx->ec_scal.p, lens, (size_t)n * 4)) return rc;
     }
     FLM_HIP(ctx, flm::launch_hash_to_curve(msgs ? ctx->ec_in.as<uint8_t>() : nullptr,
                                            msgs ? ctx->ec_scal.as<uint32_t>() : nullptr, v0, n,
                                            ctx->ec_out.as<uint8_t>(), ctx->ec_flags.as<uint32_t>(), s));
     std::vector<uint32_t> fl(n);
-    FLM_HIP(ctx, hipMemcpyAsync(fl.data(), ctx->ec_flags.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipMemcpyAsync(out, ctx->ec_out.p, (size_t)n * 64, hipMemcpyDeviceToHost, s));
-    FLM_HIP(ctx, hipStreamSynchronize(s));
+    if (int rc = hc.out(fl.data(), ctx->ec_flags.p, (size_t)n * 4)) return rc;
+    if (int rc = hc.out(out, ctx->ec_out.p, (size_t)n * 64)) return rc;
+    if (int rc = hc.finish()) return rc;
     if (flags_out) std::copy(fl.begin(), fl.end(), flags_out);
     for (int i = 0; i < n; ++i)
         if (fl[i] & 8u) return fail(ctx, FLM_EINVAL, "message %d: map_to_curve found no square root", i);

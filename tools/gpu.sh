@@ -127,7 +127,7 @@ for step in "$@"; do
       # KFD's per-process queue-eviction counter (sysfs evicted_ms) around every server unmask of the
       # c5 agent run (tools/probes/evict_probe_run.py), 3 runs x 3 iterations
       ls /sys/class/kfd/kfd 2>&1 | head; ls /sys/class/kfd/kfd/proc 2>&1 | head
-      for v in 1 2 3; do
+      for v in 1 2 3 4 5; do
         timeout -k 10 300 python -u tools/probes/evict_probe_run.py -c flamingo -n 4096 --vector_len 1048576 -i 3 \
           --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_evict_$v.log" 2>&1 || { tail -30 "$O/${TAG}_evict_$v.log"; exit 1; }
         echo "== run $v"; grep -h "evict_probe" "$O/${TAG}_evict_$v.log" | cut -c1-400
@@ -144,6 +144,23 @@ for step in "$@"; do
         cat "$O/${TAG}_thp_$v.log" >> "$O/${TAG}_thp_all.txt"
       done
       grep -h "thp_\|compact_\|pgmigrate" /proc/vmstat > "$O/${TAG}_vmstat_after.txt" 2>/dev/null; true ;;
+    pinprobe)
+      # the HIP runtime's own log of the host-pointer calls' copies: pinned (the caller's pages registered
+      # with the driver) or staged (tools/probes/pin_probe.py)
+      env $PINENV AMD_LOG_LEVEL=4 timeout -k 10 120 python -u tools/probes/pin_probe.py > "$O/${TAG}_pin_probe.out" 2> "$O/${TAG}_pin_probe.err" \
+        || { tail -20 "$O/${TAG}_pin_probe.err"; exit 1; }
+      grep -h "===\|Pinned resource\|Staging resource\|Unpinned\|staging\|hsa_amd_memory_lock\|Pin" "$O/${TAG}_pin_probe.out" "$O/${TAG}_pin_probe.err" \
+        | cut -c1-220 | head -60 > "$O/${TAG}_pin_probe_summary.txt"; cat "$O/${TAG}_pin_probe_summary.txt"; rm -f "$O/${TAG}_pin_probe.err" ;;
+    stallpin)
+      # the eviction counter with the HIP runtime never pinning the caller's pageable memory for a copy
+      # (GPU_PINNED_MIN_XFER_SIZE, MB: every pageable copy staged through the runtime's own buffers) vs default
+      for v in nopin base nopin base nopin nopin; do
+        if [ $v = nopin ]; then envs="GPU_PINNED_MIN_XFER_SIZE=1048576"; else envs=""; fi
+        env $envs timeout -k 10 300 python -u tools/probes/evict_probe_run.py -c flamingo -n 4096 --vector_len 1048576 -i 3 \
+          --dropout 0.01 --latency deterministic -k -s 5 > "$O/${TAG}_pin_$v.log" 2>&1 || { tail -30 "$O/${TAG}_pin_$v.log"; exit 1; }
+        echo "== $v"; grep -h "evict_probe\] unmask" "$O/${TAG}_pin_$v.log" | cut -c1-60
+        cat "$O/${TAG}_pin_$v.log" >> "$O/${TAG}_pin_all.txt"
+      done ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \
