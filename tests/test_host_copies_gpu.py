@@ -1,0 +1,74 @@
+"""The host-pointer entry points never hand the caller's pageable memory to a HIP copy (DESIGN.md
+section 6).  For a large pageable copy the HIP runtime pins the caller's pages (a KFD userptr
+allocation); their later unmapping made the driver evict all of the process's GPU queues for
+20-40 ms -- the agent run's unmask stall.  The library now copies through a pinned bounce buffer.
+
+The check runs every host-pointer entry point with inputs and outputs of 1-16 MiB in a child
+process under AMD_LOG_LEVEL=4 (the runtime logs "HSA Copy Using Pinned resource" when it pins a
+caller buffer for a copy) and asserts that no such line appears, while the results stay exact."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT + "/oracle")
+import oracle as O
+from flamingo_amd import MaskEngine
+eng = MaskEngine(0)
+g = np.random.Generator(np.random.PCG64(7))
+L = 1 << 20
+seeds = g.integers(0, 256, (4, 32), dtype=np.uint8)
+signs = np.array([1, -1, 1, -1], np.int8)
+rows = g.integers(0, 2**32, (4, L), dtype=np.uint32)
+print("== aggregate_unmask", flush=True)
+out = eng.aggregate_unmask(rows, seeds, signs)
+assert np.array_equal(out[:4096], O.aggregate_unmask(rows[:, :4096], seeds, signs, L=4096))
+print("== client_mask", flush=True)
+y = eng.client_mask(np.array([0, 4], np.int64), seeds, signs, L, x=rows[:1])
+assert np.array_equal(y[0, :4096], O.client_mask(np.array([0, 4], np.int64), seeds, signs, 4096, x=rows[:1, :4096])[0])
+print("== prg_expand", flush=True)
+e = eng.prg_expand(seeds, L)
+assert np.array_equal(e[3, -4096:], O.prg(seeds[3].tobytes(), 4096, L - 4096))
+print("== mask_accumulate", flush=True)
+acc = rows[1].copy()
+eng.mask_accumulate(seeds, signs, acc)
+assert np.array_equal(acc[:4096], O.aggregate_unmask(rows[1:2, :4096], seeds, signs, L=4096))
+print("== chacha20", flush=True)
+data = bytes(g.integers(0, 256, 4 << 20, dtype=np.uint8))
+ct = eng.chacha20_encrypt(seeds[0].tobytes(), data)
+assert eng.chacha20_encrypt(seeds[0].tobytes(), ct) == data
+print("== hash_to_curve_decimal", flush=True)
+pts, fl = eng.hash_to_curve_decimal(0, 1 << 16)
+assert not fl.any() and pts.shape == (1 << 16, 64)
+print("== ec_mul_wire", flush=True)
+n = 20000
+out, fl = eng.ec_mul_wire(np.repeat(pts[:1], n, axis=0), g.integers(0, 256, (n, 32), dtype=np.uint8))
+assert not (fl & 2).any()
+print("== ec_combine_wire", flush=True)
+T, D = 20, 1000
+eng.ec_combine_wire(pts[:D], np.repeat(pts[None, 1:D + 1], T, axis=0), g.integers(0, 128, (T, 32), dtype=np.uint8))
+print("== shamir_combine", flush=True)
+eng.shamir_combine([[int(v) for v in g.integers(1, 2**62, 5000)] for _ in range(20)],
+                   [int(v) for v in g.integers(1, 2**62, 20)])
+print("== done", flush=True)
+"""
+
+
+def test_host_pointer_calls_never_pin_caller_memory():
+    env = dict(os.environ, AMD_LOG_LEVEL="4")
+    r = subprocess.run([sys.executable, "-c", CHILD.replace("ROOT", repr(ROOT))], capture_output=True, text=True,
+                       timeout=110, env=env)
+    log = r.stdout + r.stderr
+    assert r.returncode == 0, log[-3000:]
+    assert "== done" in r.stdout
+    pinned = [ln for ln in log.splitlines() if "Using Pinned resource" in ln]
+    assert not pinned, "the HIP runtime pinned caller memory:\n" + "\n".join(pinned[:10])
