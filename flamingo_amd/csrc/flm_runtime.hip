@@ -997,20 +997,31 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
     return 0;
 }
 
-// The host-pointer entry points move the caller's arrays through the context's pinned bounce
-// buffer (ctx->bounce), never straight between a HIP copy and the caller's pageable pages.  For a
-// large pageable copy the HIP runtime pins those pages for the DMA (a KFD userptr allocation; its log:
-// "HSA Copy Using Pinned resource"); when the process later unmaps them (a numpy array freed), the
-// driver evicts ALL of the process's GPU queues while it revalidates: 20-40 ms in which nothing of
-// ours runs.  That was the agent run's unmask stall (the driver's per-process
-// evicted_ms grows by exactly the stall, and the stalls go away when the runtime never pins,
-// GPU_PINNED_MIN_XFER_SIZE).  One bounce buffer per context: these calls are synchronous (or, for a
-// group's ranks, synchronised before the call returns), so a call reuses it only after the last
-// call's copies out of it have completed; reserve() sizes it for the whole call before its first copy.
+// How the host-pointer entry points move the caller's arrays.  Never with a linear hipMemcpyAsync
+// straight to or from the caller's pageable pages: for a large one the HIP runtime pins those pages
+// for the DMA (a KFD userptr allocation; its log: "HSA Copy Using Pinned resource"), and when the
+// process later unmaps them (a numpy array freed) the driver evicts ALL of the process's GPU queues
+// while it revalidates: 20-40 ms in which nothing of ours runs.  That was the agent run's unmask
+// stall (the driver's per-process evicted_ms grows by exactly the stall, and
+// the stalls go away when the runtime never pins, GPU_PINNED_MIN_XFER_SIZE).
+//  - copies under kRectMin go through the context's pinned bounce buffer (ctx->bounce): a memcpy
+//    and an asynchronous DMA, no runtime staging round trip for a seed list;
+//  - larger ones go through the runtime's rect path (hipMemcpy2DAsync, in pieces of at most
+//    kRectPiece), which stages pageable memory through the runtime's own pinned buffers and never
+//    registers the caller's pages ("Unpinned write/read rect path" at AMD_LOG_LEVEL=4, 4 MiB to
+//    512 MiB, profiles/r06_rect_probe*.txt; tests/test_host_copies_gpu.py asserts it for every
+//    entry point).  It overlaps its CPU copies with the DMA: 4 MiB each way in 166 us, against
+//    369 us through a bounce buffer (memcpy, DMA, memcpy; tools/probes/bounce_probe.hip).
+// One bounce buffer per context: these calls are synchronous (or, for a group's ranks, synchronised
+// before the call returns), so a call reuses it only after the last call's copies out of it have
+// completed; reserve() sizes it for the whole call before its first copy.
 class HostCopies {
   public:
     HostCopies(flm_ctx *ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
-    static size_t room(size_t n) { return round_up(n, 256); }
+    static constexpr size_t kRectMin = size_t(64) << 10;
+    static constexpr size_t kRectPiece = size_t(256) << 20;
+    // bounce bytes of one copy of n bytes (0 for the rect path)
+    static size_t room(size_t n) { return n >= kRectMin ? 0 : round_up(n, 256); }
     int reserve(size_t bytes) {  // the sum of room(n) over the call's copies
         if (bytes > ctx_->bounce_cap) {
             if (ctx_->bounce) (void)hipHostFree(ctx_->bounce);  // waits for the device: nothing reads it after
@@ -1024,36 +1035,30 @@ class HostCopies {
         cap_ = bytes;
         return 0;
     }
-    // d_dst <- h_src (n bytes): copied into the bounce buffer now, DMA enqueued on the stream
-    int in(void *d_dst, const void *h_src, size_t n) {
-        if (!n) return 0;
-        uint8_t *b = take(n);
-        if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", n, cap_);
-        std::memcpy(b, h_src, n);
-        FLM_HIP(ctx_, hipMemcpyAsync(d_dst, b, n, hipMemcpyHostToDevice, s_));
-        return 0;
-    }
+    // d_dst <- h_src (n bytes)
+    int in(void *d_dst, const void *h_src, size_t n) { return in2d(d_dst, n, h_src, n, n, 1); }
     // rows x width bytes, host rows at h_pitch, device rows at d_pitch
     int in2d(void *d_dst, size_t d_pitch, const void *h_src, size_t h_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
+        if (width * rows >= kRectMin) return rect(d_dst, d_pitch, h_src, h_pitch, width, rows, hipMemcpyHostToDevice);
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
         for (size_t r = 0; r < rows; ++r) std::memcpy(b + r * width, static_cast<const uint8_t *>(h_src) + r * h_pitch, width);
         FLM_HIP(ctx_, hipMemcpy2DAsync(d_dst, d_pitch, b, width, width, rows, hipMemcpyHostToDevice, s_));
         return 0;
     }
-    // h_dst <- d_src: DMA into the bounce buffer now, handed to the caller by finish()
+    // h_dst <- d_src; a bounce-buffer output is handed to the caller by finish()
     int out(void *h_dst, const void *d_src, size_t n) { return out2d(h_dst, n, d_src, n, n, 1); }
     int out2d(void *h_dst, size_t h_pitch, const void *d_src, size_t d_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
+        if (width * rows >= kRectMin) return rect(h_dst, h_pitch, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost);
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
-        FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(b, d_src, width, hipMemcpyDeviceToHost, s_)
-                                : hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
+        FLM_HIP(ctx_, hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
         outs_.push_back({h_dst, h_pitch, b, width, rows});
         return 0;
     }
-    // wait for the stream, then copy the outputs to the caller
+    // wait for the stream, then copy the bounce-buffer outputs to the caller
     int finish() {
         FLM_HIP(ctx_, hipStreamSynchronize(s_));
         for (const Out &o : outs_)
@@ -1070,6 +1075,24 @@ class HostCopies {
         const uint8_t *src;
         size_t width, rows;
     };
+    // the runtime's rect path, in pieces of at most kRectPiece bytes (whole rows, or one row's columns)
+    int rect(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows, hipMemcpyKind kind) {
+        auto *d = static_cast<uint8_t *>(dst);
+        const auto *h = static_cast<const uint8_t *>(src);
+        if (width > kRectPiece) {
+            for (size_t r = 0; r < rows; ++r)
+                for (size_t c = 0; c < width; c += kRectPiece) {
+                    const size_t w = std::min(kRectPiece, width - c);
+                    FLM_HIP(ctx_, hipMemcpy2DAsync(d + r * dpitch + c, w, h + r * spitch + c, w, w, 1, kind, s_));
+                }
+            return 0;
+        }
+        const size_t per = kRectPiece / width;
+        for (size_t r0 = 0; r0 < rows; r0 += per)
+            FLM_HIP(ctx_, hipMemcpy2DAsync(d + r0 * dpitch, dpitch, h + r0 * spitch, spitch, width,
+                                           std::min(per, rows - r0), kind, s_));
+        return 0;
+    }
     uint8_t *take(size_t n) {
         if (off_ + room(n) > cap_) return nullptr;
         uint8_t *b = static_cast<uint8_t *>(ctx_->bounce) + off_;

@@ -1,9 +1,12 @@
 """The host-pointer entry points never hand the caller's pageable memory to a HIP copy (DESIGN.md
 section 6).  For a large pageable copy the HIP runtime pins the caller's pages (a KFD userptr
 allocation); their later unmapping made the driver evict all of the process's GPU queues for
-20-40 ms -- the agent run's unmask stall.  The library now copies through a pinned bounce buffer.
+20-40 ms -- the agent run's unmask stall.  The library now copies small arrays through a pinned
+bounce buffer and large ones through the runtime's rect path (hipMemcpy2DAsync), which stages them
+through the runtime's own pinned buffers.
 
-The check runs every host-pointer entry point with inputs and outputs of 1-16 MiB in a child
+The check runs every host-pointer entry point with inputs and outputs of 1 KiB-300 MiB (the 300 MiB
+output crosses the 256 MiB piece size of the rect copies) in a child
 process under AMD_LOG_LEVEL=4 (the runtime logs "HSA Copy Using Pinned resource" when it pins a
 caller buffer for a copy) and asserts that no such line appears, while the results stay exact."""
 import os
@@ -38,6 +41,12 @@ assert np.array_equal(y[0, :4096], O.client_mask(np.array([0, 4], np.int64), see
 print("== prg_expand", flush=True)
 e = eng.prg_expand(seeds, L)
 assert np.array_equal(e[3, -4096:], O.prg(seeds[3].tobytes(), 4096, L - 4096))
+print("== prg_expand 300 MiB", flush=True)
+big = g.integers(0, 256, (75, 32), dtype=np.uint8)
+e = eng.prg_expand(big, L)
+for k in (0, 63, 64, 74):
+    assert np.array_equal(e[k, -1024:], O.prg(big[k].tobytes(), 1024, L - 1024))
+del e
 print("== mask_accumulate", flush=True)
 acc = rows[1].copy()
 eng.mask_accumulate(seeds, signs, acc)

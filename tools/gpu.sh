@@ -161,6 +161,15 @@ for step in "$@"; do
         echo "== $v"; grep -h "evict_probe\] unmask" "$O/${TAG}_pin_$v.log" | cut -c1-60
         cat "$O/${TAG}_pin_$v.log" >> "$O/${TAG}_pin_all.txt"
       done ;;
+    hostab)
+      # host-pointer entry points' wall time per call: this build against the pre-bounce build (lib_v)
+      for v in new simple old new simple old; do
+        envs=""
+        if [ $v = old ]; then envs="FLM_LIB_PATH=$R/flamingo_amd/lib_v/libflamingo_hip_pre_bounce.so"; fi
+        if [ $v = simple ]; then envs="FLM_LIB_PATH=$R/flamingo_amd/lib_v/libflamingo_hip_bounce_simple.so"; fi
+        env $envs timeout -k 10 200 python -u tools/probes/host_path_ab.py > "$O/${TAG}_hostab_$v.log" 2>&1 || { tail -20 "$O/${TAG}_hostab_$v.log"; exit 1; }
+        cat "$O/${TAG}_hostab_$v.log" | grep -v amdgpu.ids
+      done ;;
     simc3)
       # BASELINE c3 through the agents: n = 1024, -o 2, L = 2^18
       timeout -k 10 900 python -u -m flamingo_amd.abides -c flamingo -n 1024 -o 2 --vector_len 262144 -i 2 -k -s 3 \
