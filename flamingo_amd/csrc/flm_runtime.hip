@@ -12,8 +12,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -125,6 +129,88 @@ struct SeedTable {
     uint64_t last_use = 0;
 };
 
+// Host copies between the caller's pageable arrays and the pinned bounce buffer (HostCopies), split
+// over a context's few worker threads and the calling thread: a 4 MiB in + 4 MiB out client mask
+// takes 0.34 ms of wall this way against 0.47 ms with one thread (profiles/r06_host_path_ab.txt).
+// Cutting the copies into 1 MiB pieces pipelined with the DMA, with workers spinning between pieces,
+// measured the same (0.34 ms) and was dropped.  Workers start lazily, on the first large copy.
+class CopyPool {
+  public:
+    static constexpr int kWorkers = 3;                      // + the calling thread
+    static constexpr size_t kMinSplit = size_t(256) << 10;  // below it the calling thread copies alone
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        work_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    // rows x width bytes, src rows at spitch, dst rows at dpitch; returns once every byte is copied
+    void copy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows) {
+        const size_t n = width * rows;
+        if (n < kMinSplit) return part(dst, dpitch, src, spitch, width, 0, n);
+        if (th_.empty())
+            for (int i = 0; i < kWorkers; ++i) th_.emplace_back([this, i] { run(i + 1); });
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = {dst, dpitch, src, spitch, width, n};
+            pending_ = kWorkers;
+            ++gen_;
+        }
+        work_.notify_all();
+        slice(0);
+        std::unique_lock<std::mutex> l(m_);
+        done_.wait(l, [this] { return pending_ == 0; });
+    }
+
+  private:
+    struct Job {
+        void *dst;
+        size_t dpitch;
+        const void *src;
+        size_t spitch, width, n;
+    };
+    // bytes [b, e) of the packed rows x width range
+    static void part(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t b, size_t e) {
+        while (b < e) {
+            const size_t r = b / width, c = b % width, m = std::min(width - c, e - b);
+            std::memcpy(static_cast<uint8_t *>(dst) + r * dpitch + c, static_cast<const uint8_t *>(src) + r * spitch + c, m);
+            b += m;
+        }
+    }
+    void slice(int i) {  // slice i of kWorkers + 1, 4 KiB-aligned bounds
+        const size_t per = ((job_.n + kWorkers) / (kWorkers + 1) + 4095) / 4096 * 4096;
+        const size_t b = std::min(job_.n, per * i), e = std::min(job_.n, b + per);
+        part(job_.dst, job_.dpitch, job_.src, job_.spitch, job_.width, b, e);
+    }
+    void run(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> l(m_);
+                work_.wait(l, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            slice(i);
+            bool last;
+            {
+                std::lock_guard<std::mutex> g(m_);
+                last = --pending_ == 0;
+            }
+            if (last) done_.notify_one();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable work_, done_;
+    std::vector<std::thread> th_;
+    Job job_{};
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 // flm_last_plan's variant for a round run by small_round_kernel (items = its workgroups)
@@ -179,6 +265,7 @@ struct flm_ctx {
     int n_cus = 0;               // the device's CU count (flm_init)
     void *bounce = nullptr;      // pinned bounce buffer of the host-pointer entry points (HostCopies)
     size_t bounce_cap = 0;
+    CopyPool copies;             // the CPU side of HostCopies' bounce-buffer copies
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
 };
 
@@ -997,31 +1084,23 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
     return 0;
 }
 
-// How the host-pointer entry points move the caller's arrays.  Never with a linear hipMemcpyAsync
-// straight to or from the caller's pageable pages: for a large one the HIP runtime pins those pages
-// for the DMA (a KFD userptr allocation; its log: "HSA Copy Using Pinned resource"), and when the
-// process later unmaps them (a numpy array freed) the driver evicts ALL of the process's GPU queues
-// while it revalidates: 20-40 ms in which nothing of ours runs.  That was the agent run's unmask
-// stall (the driver's per-process evicted_ms grows by exactly the stall, and
-// the stalls go away when the runtime never pins, GPU_PINNED_MIN_XFER_SIZE).
-//  - copies under kRectMin go through the context's pinned bounce buffer (ctx->bounce): a memcpy
-//    and an asynchronous DMA, no runtime staging round trip for a seed list;
-//  - larger ones go through the runtime's rect path (hipMemcpy2DAsync, in pieces of at most
-//    kRectPiece), which stages pageable memory through the runtime's own pinned buffers and never
-//    registers the caller's pages ("Unpinned write/read rect path" at AMD_LOG_LEVEL=4, 4 MiB to
-//    512 MiB, profiles/r06_rect_probe*.txt; tests/test_host_copies_gpu.py asserts it for every
-//    entry point).  It overlaps its CPU copies with the DMA: 4 MiB each way in 166 us, against
-//    369 us through a bounce buffer (memcpy, DMA, memcpy; tools/probes/bounce_probe.hip).
-// One bounce buffer per context: these calls are synchronous (or, for a group's ranks, synchronised
-// before the call returns), so a call reuses it only after the last call's copies out of it have
-// completed; reserve() sizes it for the whole call before its first copy.
+// The host-pointer entry points move the caller's arrays through the context's pinned bounce
+// buffer (ctx->bounce), never straight between a HIP copy and the caller's pageable pages.  For a
+// large pageable copy the HIP runtime pins those pages for the DMA (a KFD userptr allocation; its log:
+// "HSA Copy Using Pinned resource"); when the process later unmaps them (a numpy array freed), the
+// driver evicts ALL of the process's GPU queues while it revalidates: 20-40 ms in which nothing of
+// ours runs.  That was the agent run's unmask stall (the driver's per-process
+// evicted_ms grows by exactly the stall, and the stalls go away when the runtime never pins,
+// GPU_PINNED_MIN_XFER_SIZE).  The runtime's rect path (hipMemcpy2DAsync) logs no pinning but brings
+// the evictions back all the same (5 of 5 runs, profiles/r06_rect_path_evictions.log), so every
+// caller array, small or large, goes through the bounce buffer; the CPU side of the copies is split
+// over the context's CopyPool.  One bounce buffer per context: these calls are synchronous (or, for a
+// group's ranks, synchronised before the call returns), so a call reuses it only after the last
+// call's copies out of it have completed; reserve() sizes it for the whole call before its first copy.
 class HostCopies {
   public:
     HostCopies(flm_ctx *ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
-    static constexpr size_t kRectMin = size_t(64) << 10;
-    static constexpr size_t kRectPiece = size_t(256) << 20;
-    // bounce bytes of one copy of n bytes (0 for the rect path)
-    static size_t room(size_t n) { return n >= kRectMin ? 0 : round_up(n, 256); }
+    static size_t room(size_t n) { return round_up(n, 256); }
     int reserve(size_t bytes) {  // the sum of room(n) over the call's copies
         if (bytes > ctx_->bounce_cap) {
             if (ctx_->bounce) (void)hipHostFree(ctx_->bounce);  // waits for the device: nothing reads it after
@@ -1035,35 +1114,33 @@ class HostCopies {
         cap_ = bytes;
         return 0;
     }
-    // d_dst <- h_src (n bytes)
+    // d_dst <- h_src (n bytes): copied into the bounce buffer now, DMA enqueued on the stream
     int in(void *d_dst, const void *h_src, size_t n) { return in2d(d_dst, n, h_src, n, n, 1); }
     // rows x width bytes, host rows at h_pitch, device rows at d_pitch
     int in2d(void *d_dst, size_t d_pitch, const void *h_src, size_t h_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
-        if (width * rows >= kRectMin) return rect(d_dst, d_pitch, h_src, h_pitch, width, rows, hipMemcpyHostToDevice);
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
-        for (size_t r = 0; r < rows; ++r) std::memcpy(b + r * width, static_cast<const uint8_t *>(h_src) + r * h_pitch, width);
-        FLM_HIP(ctx_, hipMemcpy2DAsync(d_dst, d_pitch, b, width, width, rows, hipMemcpyHostToDevice, s_));
+        ctx_->copies.copy2d(b, width, h_src, h_pitch, width, rows);
+        FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(d_dst, b, width, hipMemcpyHostToDevice, s_)
+                                : hipMemcpy2DAsync(d_dst, d_pitch, b, width, width, rows, hipMemcpyHostToDevice, s_));
         return 0;
     }
-    // h_dst <- d_src; a bounce-buffer output is handed to the caller by finish()
+    // h_dst <- d_src: DMA into the bounce buffer now, handed to the caller by finish()
     int out(void *h_dst, const void *d_src, size_t n) { return out2d(h_dst, n, d_src, n, n, 1); }
     int out2d(void *h_dst, size_t h_pitch, const void *d_src, size_t d_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
-        if (width * rows >= kRectMin) return rect(h_dst, h_pitch, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost);
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
-        FLM_HIP(ctx_, hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
+        FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(b, d_src, width, hipMemcpyDeviceToHost, s_)
+                                : hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
         outs_.push_back({h_dst, h_pitch, b, width, rows});
         return 0;
     }
-    // wait for the stream, then copy the bounce-buffer outputs to the caller
+    // wait for the stream, then copy the outputs to the caller
     int finish() {
         FLM_HIP(ctx_, hipStreamSynchronize(s_));
-        for (const Out &o : outs_)
-            for (size_t r = 0; r < o.rows; ++r)
-                std::memcpy(static_cast<uint8_t *>(o.dst) + r * o.pitch, o.src + r * o.width, o.width);
+        for (const Out &o : outs_) ctx_->copies.copy2d(o.dst, o.pitch, o.src, o.width, o.width, o.rows);
         outs_.clear();
         return 0;
     }
@@ -1075,24 +1152,6 @@ class HostCopies {
         const uint8_t *src;
         size_t width, rows;
     };
-    // the runtime's rect path, in pieces of at most kRectPiece bytes (whole rows, or one row's columns)
-    int rect(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows, hipMemcpyKind kind) {
-        auto *d = static_cast<uint8_t *>(dst);
-        const auto *h = static_cast<const uint8_t *>(src);
-        if (width > kRectPiece) {
-            for (size_t r = 0; r < rows; ++r)
-                for (size_t c = 0; c < width; c += kRectPiece) {
-                    const size_t w = std::min(kRectPiece, width - c);
-                    FLM_HIP(ctx_, hipMemcpy2DAsync(d + r * dpitch + c, w, h + r * spitch + c, w, w, 1, kind, s_));
-                }
-            return 0;
-        }
-        const size_t per = kRectPiece / width;
-        for (size_t r0 = 0; r0 < rows; r0 += per)
-            FLM_HIP(ctx_, hipMemcpy2DAsync(d + r0 * dpitch, dpitch, h + r0 * spitch, spitch, width,
-                                           std::min(per, rows - r0), kind, s_));
-        return 0;
-    }
     uint8_t *take(size_t n) {
         if (off_ + room(n) > cap_) return nullptr;
         uint8_t *b = static_cast<uint8_t *>(ctx_->bounce) + off_;
