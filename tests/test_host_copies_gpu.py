@@ -37,6 +37,11 @@ assert np.array_equal(out, O.aggregate_unmask(rows, seeds, signs, L=L))
 print("== client_mask", flush=True)
 y = eng.client_mask(np.array([0, 4], np.int64), seeds, signs, L, x=rows[:1])
 assert np.array_equal(y, O.client_mask(np.array([0, 4], np.int64), seeds, signs, L, x=rows[:1]))
+print("== client_mask 3 ragged rows", flush=True)
+L2 = 100_003  # device rows padded to a wider pitch: 2-D copies whose thread slices cross rows
+x3 = g.integers(0, 2**32, (3, L2), dtype=np.uint32)
+seg3 = np.array([0, 2, 3, 4], np.int64)
+assert np.array_equal(eng.client_mask(seg3, seeds, signs, L2, x=x3), O.client_mask(seg3, seeds, signs, L2, x=x3))
 print("== prg_expand", flush=True)
 e = eng.prg_expand(seeds, L)
 assert all(np.array_equal(e[k], O.prg(seeds[k].tobytes(), L, 0)) for k in range(4))
