@@ -22,6 +22,12 @@
 #   prof         rocprofv3 kernel trace + stats and PMC passes of bench.py --profile (gpu_prof.sh)
 #   clock        PMC clock/CPI passes (gpu_clock.sh)
 #   py:SCRIPT[:ARG]  python tools/SCRIPT [ARG] (e.g. probes/recon_partial_sweep.py) -> gpurun_out/TAG_<name>.log
+#   expand       tools/expand_bench.py (the prg_expand leg alone)
+#   stallab / stallscr / stallnuma / stallthp / stallpin / pinprobe / stallevict
+#                round 6's unmask-stall diagnosis: c5 agent runs with the HIP API
+#                trace, scratch / NUMA / THP / pinning settings, the runtime's copy log, and KFD's
+#                per-process evicted_ms around every unmask (stallevict: 5 runs x 3 iterations)
+#   hostab       tools/probes/host_path_ab.py: host-pointer calls' wall time, this build against lib_v/
 TAG=${1:?usage: tools/gpu.sh TAG STEP...}
 shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
