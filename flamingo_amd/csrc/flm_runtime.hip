@@ -994,6 +994,19 @@ bool host_pinned(const void *p) {
 // (HostCopies below says why).
 constexpr size_t kStageBytes = 32u << 20;
 
+// The two kStageBytes pinned staging buffers of the context (upload_rows, HostCopies' large copies).
+int ensure_stage(flm_ctx *ctx) {
+    if (ctx->stage_cap >= kStageBytes) return 0;
+    for (int b = 0; b < 2; ++b) {
+        if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
+        ctx->stage[b] = nullptr;
+        FLM_HIP(ctx, hipHostMalloc(&ctx->stage[b], kStageBytes, hipHostMallocDefault));
+        if (!ctx->stage_done[b]) FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->stage_done[b], hipEventDisableTiming));
+    }
+    ctx->stage_cap = kStageBytes;
+    return 0;
+}
+
 int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint64_t pitch) {
     FLM_HIP(ctx, ctx->rows.reserve(std::max<size_t>(1, (size_t)N) * pitch * sizeof(uint32_t)));
     uint32_t *dst = ctx->rows.as<uint32_t>();
@@ -1037,15 +1050,7 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
         }
     }
     if (pageable.empty()) return 0;
-    if (ctx->stage_cap < kStageBytes) {
-        for (int b = 0; b < 2; ++b) {
-            if (ctx->stage[b]) (void)hipHostFree(ctx->stage[b]);
-            ctx->stage[b] = nullptr;
-            FLM_HIP(ctx, hipHostMalloc(&ctx->stage[b], kStageBytes, hipHostMallocDefault));
-            if (!ctx->stage_done[b]) FLM_HIP(ctx, hipEventCreateWithFlags(&ctx->stage_done[b], hipEventDisableTiming));
-        }
-        ctx->stage_cap = kStageBytes;
-    }
+    if (int rc = ensure_stage(ctx)) return rc;
     size_t k = 0;
     int b = 0;
     bool used[2] = {false, false};
@@ -1054,7 +1059,7 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
             for (size_t off = 0; off < row_bytes; off += kStageBytes) {
                 const size_t n = std::min(kStageBytes, row_bytes - off);
                 if (used[b]) FLM_HIP(ctx, hipEventSynchronize(ctx->stage_done[b]));
-                std::memcpy(ctx->stage[b], reinterpret_cast<const uint8_t *>(rows[i]) + off, n);
+                ctx->copies.copy2d(ctx->stage[b], n, reinterpret_cast<const uint8_t *>(rows[i]) + off, n, n, 1);
                 FLM_HIP(ctx, hipMemcpyAsync(reinterpret_cast<uint8_t *>(dst + (size_t)i * pitch) + off, ctx->stage[b], n,
                                             hipMemcpyHostToDevice, ctx->stream));
                 FLM_HIP(ctx, hipEventRecord(ctx->stage_done[b], ctx->stream));
@@ -1071,7 +1076,7 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
         const int first = pageable[k];
         size_t n = 0;
         while (k + n < pageable.size() && n < per_buf && pageable[k + n] == first + (int)n) {
-            std::memcpy(st + n * slot_bytes, rows[pageable[k + n]], row_bytes);
+            ctx->copies.copy2d(st + n * slot_bytes, row_bytes, rows[pageable[k + n]], row_bytes, row_bytes, 1);
             ++n;
         }
         FLM_HIP(ctx, hipMemcpyAsync(dst + (size_t)first * pitch, st, n * slot_bytes - (slot_bytes - row_bytes),
@@ -1097,10 +1102,13 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
 // over the context's CopyPool.  One bounce buffer per context: these calls are synchronous (or, for a
 // group's ranks, synchronised before the call returns), so a call reuses it only after the last
 // call's copies out of it have completed; reserve() sizes it for the whole call before its first copy.
+// Copies of kStageBytes or more skip it and stream through the context's two staging buffers instead
+// (inputs at once, outputs in finish()), so no call pins more host memory than its small copies plus
+// 2 x 32 MiB, whatever its size (a 962 x 2^20 prg_expand returns 4 GiB).
 class HostCopies {
   public:
     HostCopies(flm_ctx *ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
-    static size_t room(size_t n) { return round_up(n, 256); }
+    static size_t room(size_t n) { return n >= kStageBytes ? 0 : round_up(n, 256); }
     int reserve(size_t bytes) {  // the sum of room(n) over the call's copies
         if (bytes > ctx_->bounce_cap) {
             if (ctx_->bounce) (void)hipHostFree(ctx_->bounce);  // waits for the device: nothing reads it after
@@ -1119,6 +1127,7 @@ class HostCopies {
     // rows x width bytes, host rows at h_pitch, device rows at d_pitch
     int in2d(void *d_dst, size_t d_pitch, const void *h_src, size_t h_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
+        if (width * rows >= kStageBytes) return stream_in(d_dst, d_pitch, h_src, h_pitch, width, rows);
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
         ctx_->copies.copy2d(b, width, h_src, h_pitch, width, rows);
@@ -1130,6 +1139,10 @@ class HostCopies {
     int out(void *h_dst, const void *d_src, size_t n) { return out2d(h_dst, n, d_src, n, n, 1); }
     int out2d(void *h_dst, size_t h_pitch, const void *d_src, size_t d_pitch, size_t width, size_t rows) {
         if (!width || !rows) return 0;
+        if (width * rows >= kStageBytes) {
+            bigs_.push_back({h_dst, h_pitch, static_cast<const uint8_t *>(d_src), d_pitch, width, rows});
+            return 0;
+        }
         uint8_t *b = take(width * rows);
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
         FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(b, d_src, width, hipMemcpyDeviceToHost, s_)
@@ -1137,11 +1150,14 @@ class HostCopies {
         outs_.push_back({h_dst, h_pitch, b, width, rows});
         return 0;
     }
-    // wait for the stream, then copy the outputs to the caller
+    // wait for the stream, then copy the outputs to the caller (large ones through the staging ring)
     int finish() {
         FLM_HIP(ctx_, hipStreamSynchronize(s_));
         for (const Out &o : outs_) ctx_->copies.copy2d(o.dst, o.pitch, o.src, o.width, o.width, o.rows);
         outs_.clear();
+        for (const Big &g : bigs_)
+            if (int rc = stream_out(g)) return rc;
+        bigs_.clear();
         return 0;
     }
 
@@ -1152,6 +1168,67 @@ class HostCopies {
         const uint8_t *src;
         size_t width, rows;
     };
+    struct Big {  // a large output: device rows at d_pitch -> host rows at h_pitch
+        void *dst;
+        size_t h_pitch;
+        const uint8_t *src;
+        size_t d_pitch, width, rows;
+    };
+    // Pieces of at most kStageBytes of a rows x width copy: whole rows, or one row's columns.
+    struct Piece {
+        size_t r, c, w, nr;  // first row, first column, bytes per row, rows
+    };
+    static std::vector<Piece> pieces(size_t width, size_t rows) {
+        std::vector<Piece> v;
+        if (width > kStageBytes) {
+            for (size_t r = 0; r < rows; ++r)
+                for (size_t c = 0; c < width; c += kStageBytes) v.push_back({r, c, std::min(kStageBytes, width - c), 1});
+        } else {
+            const size_t per = kStageBytes / width;
+            for (size_t r = 0; r < rows; r += per) v.push_back({r, 0, width, std::min(per, rows - r)});
+        }
+        return v;
+    }
+    // a large input: each piece copied into the next free staging buffer, then DMA'd from it
+    int stream_in(void *d_dst, size_t d_pitch, const void *h_src, size_t h_pitch, size_t width, size_t rows) {
+        if (int rc = ensure_stage(ctx_)) return rc;
+        const auto *src = static_cast<const uint8_t *>(h_src);
+        auto *dst = static_cast<uint8_t *>(d_dst);
+        int b = 0;
+        for (const Piece &p : pieces(width, rows)) {
+            FLM_HIP(ctx_, hipEventSynchronize(ctx_->stage_done[b]));  // the DMA out of this buffer is done
+            auto *st = static_cast<uint8_t *>(ctx_->stage[b]);
+            ctx_->copies.copy2d(st, p.w, src + p.r * h_pitch + p.c, h_pitch, p.w, p.nr);
+            FLM_HIP(ctx_, hipMemcpy2DAsync(dst + p.r * d_pitch + p.c, d_pitch, st, p.w, p.w, p.nr, hipMemcpyHostToDevice, s_));
+            FLM_HIP(ctx_, hipEventRecord(ctx_->stage_done[b], s_));
+            b ^= 1;
+        }
+        return 0;
+    }
+    // a large output, after the stream has drained: piece i + 1 lands in one staging buffer while
+    // piece i is copied out of the other
+    int stream_out(const Big &g) {
+        if (int rc = ensure_stage(ctx_)) return rc;
+        const std::vector<Piece> ps = pieces(g.width, g.rows);
+        auto issue = [&](size_t i) -> int {
+            const Piece &p = ps[i];
+            FLM_HIP(ctx_, hipMemcpy2DAsync(ctx_->stage[i & 1], p.w, g.src + p.r * g.d_pitch + p.c, g.d_pitch, p.w, p.nr,
+                                           hipMemcpyDeviceToHost, s_));
+            FLM_HIP(ctx_, hipEventRecord(ctx_->stage_done[i & 1], s_));
+            return 0;
+        };
+        for (size_t i = 0; i < ps.size() && i < 2; ++i)
+            if (int rc = issue(i)) return rc;
+        for (size_t i = 0; i < ps.size(); ++i) {
+            const Piece &p = ps[i];
+            FLM_HIP(ctx_, hipEventSynchronize(ctx_->stage_done[i & 1]));
+            ctx_->copies.copy2d(static_cast<uint8_t *>(g.dst) + p.r * g.h_pitch + p.c, g.h_pitch, ctx_->stage[i & 1], p.w,
+                                p.w, p.nr);
+            if (i + 2 < ps.size())
+                if (int rc = issue(i + 2)) return rc;
+        }
+        return 0;
+    }
     uint8_t *take(size_t n) {
         if (off_ + room(n) > cap_) return nullptr;
         uint8_t *b = static_cast<uint8_t *>(ctx_->bounce) + off_;
@@ -1162,6 +1239,7 @@ class HostCopies {
     hipStream_t s_;
     size_t cap_ = 0, off_ = 0;
     std::vector<Out> outs_;
+    std::vector<Big> bigs_;
 };
 
 size_t seeds_room(int K) { return K > 0 ? HostCopies::room((size_t)K * 32) + HostCopies::room((size_t)K) : 0; }

@@ -1,11 +1,12 @@
 """The host-pointer entry points never hand the caller's pageable memory to a HIP copy (DESIGN.md
 section 6).  For a large pageable copy the HIP runtime pins the caller's pages (a KFD userptr
 allocation); their later unmapping made the driver evict all of the process's GPU queues for
-20-40 ms -- the agent run's unmask stall.  The library now copies every caller array through a
-pinned bounce buffer (the CPU side split over the context's copy threads).
+20-40 ms -- the agent run's unmask stall.  The library now copies every caller array through
+pinned memory of its own: a bounce buffer for copies under 32 MiB, the two 32 MiB staging buffers
+in pieces for larger ones (the CPU side split over the context's copy threads).
 
-The check runs every host-pointer entry point with inputs and outputs of 1 KiB-300 MiB (the 300 MiB
-output crosses the 256 MiB piece size of the rect copies) in a child
+The check runs every host-pointer entry point with inputs and outputs of 1 KiB-300 MiB (40 MiB in
+and out: a 32 MiB piece and a tail of one row; 300 MiB out: 10 pieces of 8 rows) in a child
 process under AMD_LOG_LEVEL=4 (the runtime logs "HSA Copy Using Pinned resource" when it pins a
 caller buffer for a copy) and asserts that no such line appears, while the results stay exact."""
 import os
@@ -59,6 +60,10 @@ print("== chacha20", flush=True)
 data = bytes(g.integers(0, 256, 4 << 20, dtype=np.uint8))
 ct = eng.chacha20_encrypt(seeds[0].tobytes(), data)
 assert eng.chacha20_encrypt(seeds[0].tobytes(), ct) == data
+print("== chacha20 40 MiB", flush=True)
+data = bytes(g.integers(0, 256, 40 << 20, dtype=np.uint8))  # one 32 MiB piece + a tail, each way
+assert eng.chacha20_encrypt(seeds[1].tobytes(), data) == O.chacha20_encrypt(seeds[1].tobytes(), data)
+del data
 print("== hash_to_curve_decimal", flush=True)
 pts, fl = eng.hash_to_curve_decimal(0, 1 << 16)
 assert not fl.any() and pts.shape == (1 << 16, 64)
