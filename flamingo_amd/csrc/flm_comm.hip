@@ -592,7 +592,7 @@ int flm_group_aggregate_unmask(flm_group *g, const uint32_t *const *rows, int N,
         if (e != hipSuccess) return gfail(g, FLM_EHIP, std::string("shard D2H: ") + hipGetErrorString(e));
     }
     if (int rc = flm_group_sync(g)) return rc;
-    std::memcpy(out, g->hout, L * sizeof(uint32_t));
+    flm::rt::host_copy(g->ctx[0], out, g->hout, L * sizeof(uint32_t));
     return 0;
 }
 

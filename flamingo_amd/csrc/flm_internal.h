@@ -139,6 +139,8 @@ int set_error(flm_ctx *ctx, int code, const char *msg);
 int device_of(const flm_ctx *ctx);
 hipStream_t stream_of(const flm_ctx *ctx);
 void **comm_slot(flm_ctx *ctx);
+// n bytes between host buffers on the context's copy threads (the CPU side of a pinned-buffer copy)
+void host_copy(flm_ctx *ctx, void *dst, const void *src, size_t n);
 // The calling thread's current device belongs to the caller: every entry point that selects a
 // device (its context's, or each rank's of a group or store) gives the caller's back on return.
 // torch and the agents' own HIP code allocate on the current device, and a group call that left

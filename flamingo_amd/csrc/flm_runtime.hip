@@ -150,6 +150,7 @@ class CopyPool {
     void copy2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows) {
         const size_t n = width * rows;
         if (n < kMinSplit) return part(dst, dpitch, src, spitch, width, 0, n);
+        std::lock_guard<std::mutex> one_job(call_);  // a context's callers are one thread, a store's adds too
         if (th_.empty())
             for (int i = 0; i < kWorkers; ++i) th_.emplace_back([this, i] { run(i + 1); });
         {
@@ -202,7 +203,7 @@ class CopyPool {
             if (last) done_.notify_one();
         }
     }
-    std::mutex m_;
+    std::mutex call_, m_;
     std::condition_variable work_, done_;
     std::vector<std::thread> th_;
     Job job_{};
@@ -1354,6 +1355,7 @@ int set_error(flm_ctx *ctx, int code, const char *msg) { return fail(ctx, code, 
 int device_of(const flm_ctx *ctx) { return ctx->device; }
 hipStream_t stream_of(const flm_ctx *ctx) { return ctx->stream; }
 void **comm_slot(flm_ctx *ctx) { return &ctx->comm; }
+void host_copy(flm_ctx *ctx, void *dst, const void *src, size_t n) { ctx->copies.copy2d(dst, n, src, n, n, 1); }
 
 int host_round_async(flm_ctx *ctx, const uint32_t *const *rows, int N, const uint8_t *seeds, const int8_t *signs,
                      int K, size_t L, size_t mask_lo, size_t mask_hi, uint32_t *d_out) {

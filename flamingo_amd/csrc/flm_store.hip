@@ -262,7 +262,7 @@ int flm_store_add(flm_store *st, int64_t sender, const uint32_t *row, size_t n) 
     const int b = k.next;
     k.next = (b + 1) % kStoreRing;
     if (k.stage_busy[b]) FLM_SHIP(st, hipEventSynchronize(k.stage_done[b]));  // its last DMA has read it
-    std::memcpy(k.stage[b], row, st->L * sizeof(uint32_t));
+    flm::rt::host_copy(k.ctx, k.stage[b], row, st->L * sizeof(uint32_t));
     FLM_SHIP(st, hipMemcpyAsync(k.rows + (size_t)i * st->pitch, k.stage[b], st->L * sizeof(uint32_t),
                                 hipMemcpyHostToDevice, k.copy));
     FLM_SHIP(st, hipEventRecord(k.stage_done[b], k.copy));
@@ -346,7 +346,7 @@ int flm_store_partial_host(flm_store *st, uint32_t *out) {
         FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
     }
     st->bounce_busy = false;
-    std::memcpy(out, st->hout, st->L * sizeof(uint32_t));
+    flm::rt::host_copy(st->rk[0].ctx, out, st->hout, st->L * sizeof(uint32_t));
     return 0;
 }
 
@@ -405,7 +405,7 @@ int flm_store_unmask(flm_store *st, const uint8_t *seeds, const int8_t *signs, i
         FLM_SHIP(st, hipStreamSynchronize(flm::rt::stream_of(k.ctx)));
     }
     st->bounce_busy = false;
-    std::memcpy(out, st->hout, st->L * sizeof(uint32_t));
+    flm::rt::host_copy(st->rk[0].ctx, out, st->hout, st->L * sizeof(uint32_t));
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, st->u0, st->u1) == hipSuccess) st->unmask_ms = ms;
     return 0;
