@@ -1148,13 +1148,20 @@ class HostCopies {
         if (!b) return fail(ctx_, FLM_EINVAL, "host bounce: %zu bytes past the reserved %zu", width * rows, cap_);
         FLM_HIP(ctx_, rows == 1 ? hipMemcpyAsync(b, d_src, width, hipMemcpyDeviceToHost, s_)
                                 : hipMemcpy2DAsync(b, width, d_src, d_pitch, width, rows, hipMemcpyDeviceToHost, s_));
-        outs_.push_back({h_dst, h_pitch, b, width, rows});
+        outs_.push_back({h_dst, h_pitch, b, width, width, rows});
         return 0;
+    }
+    // n bytes of the bounce buffer for a kernel to read or write in place (the GPU reaches pinned host
+    // memory over the link), nullptr for n of kStageBytes or more: a caller then copies as above
+    uint8_t *mapped(size_t n) { return n < kStageBytes ? take(n) : nullptr; }
+    // rows x width bytes a kernel wrote in place at b (mapped) at b_pitch, to the caller's rows at h_pitch
+    void out_mapped(void *h_dst, size_t h_pitch, const uint8_t *b, size_t b_pitch, size_t width, size_t rows) {
+        outs_.push_back({h_dst, h_pitch, b, b_pitch, width, rows});
     }
     // wait for the stream, then copy the outputs to the caller (large ones through the staging ring)
     int finish() {
         FLM_HIP(ctx_, hipStreamSynchronize(s_));
-        for (const Out &o : outs_) ctx_->copies.copy2d(o.dst, o.pitch, o.src, o.width, o.width, o.rows);
+        for (const Out &o : outs_) ctx_->copies.copy2d(o.dst, o.pitch, o.src, o.spitch, o.width, o.rows);
         outs_.clear();
         for (const Big &g : bigs_)
             if (int rc = stream_out(g)) return rc;
@@ -1167,7 +1174,7 @@ class HostCopies {
         void *dst;
         size_t pitch;
         const uint8_t *src;
-        size_t width, rows;
+        size_t spitch, width, rows;
     };
     struct Big {  // a large output: device rows at d_pitch -> host rows at h_pitch
         void *dst;
@@ -1570,6 +1577,22 @@ int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, 
     const uint64_t pitch = round_up(L, 64);
     const size_t plane = (size_t)N * L * 4;
     HostCopies hc(ctx, ctx->stream);
+    const uint64_t hp = round_up(L, 4);  // pitch of the in-place planes
+    const size_t hplane = (size_t)N * hp * 4;
+    if (hplane < kStageBytes) {
+        // one client's call (c5: 4 MiB in, 4 MiB out): the kernel reads x from and writes y to the
+        // pinned bounce buffer in place, so the link carries both at once instead of a DMA each way
+        if (int rc = hc.reserve((x ? HostCopies::room(hplane) : 0) + seeds_room((int)K) + HostCopies::room(hplane))) return rc;
+        uint8_t *bx = x ? hc.mapped(hplane) : nullptr;
+        if (bx) ctx->copies.copy2d(bx, hp * 4, x, L * 4, L * 4, (size_t)N);
+        if (int rc = upload_seeds(ctx, hc, seeds, signs, (int)K)) return rc;
+        uint8_t *by = hc.mapped(hplane);
+        if (int rc = flm_client_mask_dev(ctx, reinterpret_cast<const uint32_t *>(bx), hp, N, seg, ctx->seeds.as<uint8_t>(),
+                                         signs, L, reinterpret_cast<uint32_t *>(by), ctx->stream))
+            return rc;
+        hc.out_mapped(out, L * 4, by, hp * 4, L * 4, (size_t)N);
+        return hc.finish();
+    }
     if (int rc = hc.reserve((x ? HostCopies::room(plane) : 0) + seeds_room((int)K) + HostCopies::room(plane))) return rc;
     uint32_t *d_x = nullptr;
     if (x) {
@@ -1640,9 +1663,18 @@ int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t
     FLM_ON_DEVICE(ctx);
     const uint64_t pitch = round_up(L, 64);
     HostCopies hc(ctx, ctx->stream);
-    if (int rc = hc.reserve(HostCopies::room((size_t)K * 32) + HostCopies::room((size_t)K * L * 4))) return rc;
+    const uint64_t hp = round_up(L, 4);  // pitch of rows written in place
+    if (int rc = hc.reserve(HostCopies::room((size_t)K * 32) + HostCopies::room((size_t)K * hp * 4))) return rc;
     FLM_HIP(ctx, ctx->seeds.reserve((size_t)K * 32));
     if (int rc = hc.in(ctx->seeds.p, seeds, (size_t)K * 32)) return rc;
+    if ((size_t)K * hp * 4 < kStageBytes) {  // rows written in place in the bounce buffer (flm_client_mask)
+        uint8_t *bo = hc.mapped((size_t)K * hp * 4);
+        if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, reinterpret_cast<uint32_t *>(bo), hp,
+                                        ctx->stream))
+            return rc;
+        hc.out_mapped(out, L * 4, bo, hp * 4, L * 4, (size_t)K);
+        return hc.finish();
+    }
     FLM_HIP(ctx, ctx->out.reserve((size_t)K * pitch * sizeof(uint32_t)));
     if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, ctx->out.as<uint32_t>(), pitch,
                                     ctx->stream))
@@ -1703,6 +1735,17 @@ int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs,
     const uint64_t pitch = round_up(L, 64);
     HostCopies hc(ctx, ctx->stream);
     if (int rc = hc.reserve(2 * HostCopies::room(L * 4) + seeds_room(K))) return rc;
+    if (L * 4 < kStageBytes) {  // acc read and written in place in the bounce buffer (flm_client_mask)
+        uint8_t *bx = hc.mapped(L * 4), *by = hc.mapped(L * 4);
+        ctx->copies.copy2d(bx, L * 4, acc, L * 4, L * 4, 1);
+        if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
+        if (int rc = flm_aggregate_unmask_dev(ctx, reinterpret_cast<const uint32_t *>(bx), round_up(L, 4), 1,
+                                              ctx->seeds.as<uint8_t>(), ctx->signs.as<int8_t>(), K, L, 0, L, slot0,
+                                              reinterpret_cast<uint32_t *>(by), ctx->stream))
+            return rc;
+        hc.out_mapped(acc, L * 4, by, L * 4, L * 4, 1);
+        return hc.finish();
+    }
     FLM_HIP(ctx, ctx->rows.reserve(pitch * sizeof(uint32_t)));
     if (int rc = hc.in(ctx->rows.p, acc, L * 4)) return rc;
     if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
@@ -1728,10 +1771,17 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
     for (int i = 0; i < 2; ++i)
         nn[i] = (uint32_t)nonce[4 * i] | ((uint32_t)nonce[4 * i + 1] << 8) | ((uint32_t)nonce[4 * i + 2] << 16) |
                 ((uint32_t)nonce[4 * i + 3] << 24);
-    FLM_HIP(ctx, ctx->bytes_in.reserve(n));
-    FLM_HIP(ctx, ctx->bytes_out.reserve(n));
     HostCopies hc(ctx, ctx->stream);
     if (int rc = hc.reserve(2 * HostCopies::room(n))) return rc;
+    if (n < kStageBytes) {  // read and written in place in the bounce buffer (flm_client_mask)
+        uint8_t *bi = hc.mapped(n), *bo = hc.mapped(n);
+        ctx->copies.copy2d(bi, n, in, n, n, 1);
+        FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, bi, bo, n, ctx->stream));
+        hc.out_mapped(out, n, bo, n, n, 1);
+        return hc.finish();
+    }
+    FLM_HIP(ctx, ctx->bytes_in.reserve(n));
+    FLM_HIP(ctx, ctx->bytes_out.reserve(n));
     if (int rc = hc.in(ctx->bytes_in.p, in, n)) return rc;
     FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, ctx->bytes_in.as<uint8_t>(), ctx->bytes_out.as<uint8_t>(), n,
                                           ctx->stream));
