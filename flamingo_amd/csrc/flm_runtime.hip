@@ -265,6 +265,7 @@ struct flm_ctx {
                                   // a SIMD at once, the rest queue behind them and even out the runs' ends
     int n_cus = 0;               // the device's CU count (flm_init)
     void *bounce = nullptr;      // pinned bounce buffer of the host-pointer entry points (HostCopies)
+    void *bounce_dev = nullptr;  // its address for kernels (hipHostGetDevicePointer)
     size_t bounce_cap = 0;
     CopyPool copies;             // the CPU side of HostCopies' bounce-buffer copies
     void *comm = nullptr;    // RCCL communicator state (flm_comm.hip), owned by the context
@@ -1119,6 +1120,7 @@ class HostCopies {
             const hipError_t e = hipHostMalloc(&ctx_->bounce, want, hipHostMallocDefault);
             if (e != hipSuccess) return fail(ctx_, FLM_ENOMEM, "pinned bounce buffer of %zu bytes: %s", want, hipGetErrorString(e));
             ctx_->bounce_cap = want;
+            FLM_HIP(ctx_, hipHostGetDevicePointer(&ctx_->bounce_dev, ctx_->bounce, 0));
         }
         cap_ = bytes;
         return 0;
@@ -1154,6 +1156,12 @@ class HostCopies {
     // n bytes of the bounce buffer for a kernel to read or write in place (the GPU reaches pinned host
     // memory over the link), nullptr for n of kStageBytes or more: a caller then copies as above
     uint8_t *mapped(size_t n) { return n < kStageBytes ? take(n) : nullptr; }
+    // the kernel-side address of host address b of the bounce buffer
+    template <class T>
+    T *dev(const uint8_t *b) const {
+        return b ? reinterpret_cast<T *>(static_cast<uint8_t *>(ctx_->bounce_dev) + (b - static_cast<uint8_t *>(ctx_->bounce)))
+                 : nullptr;
+    }
     // rows x width bytes a kernel wrote in place at b (mapped) at b_pitch, to the caller's rows at h_pitch
     void out_mapped(void *h_dst, size_t h_pitch, const uint8_t *b, size_t b_pitch, size_t width, size_t rows) {
         outs_.push_back({h_dst, h_pitch, b, b_pitch, width, rows});
@@ -1587,8 +1595,8 @@ int flm_client_mask(flm_ctx *ctx, const uint32_t *x, int N, const int64_t *seg, 
         if (bx) ctx->copies.copy2d(bx, hp * 4, x, L * 4, L * 4, (size_t)N);
         if (int rc = upload_seeds(ctx, hc, seeds, signs, (int)K)) return rc;
         uint8_t *by = hc.mapped(hplane);
-        if (int rc = flm_client_mask_dev(ctx, reinterpret_cast<const uint32_t *>(bx), hp, N, seg, ctx->seeds.as<uint8_t>(),
-                                         signs, L, reinterpret_cast<uint32_t *>(by), ctx->stream))
+        if (int rc = flm_client_mask_dev(ctx, hc.dev<const uint32_t>(bx), hp, N, seg, ctx->seeds.as<uint8_t>(), signs, L,
+                                         hc.dev<uint32_t>(by), ctx->stream))
             return rc;
         hc.out_mapped(out, L * 4, by, hp * 4, L * 4, (size_t)N);
         return hc.finish();
@@ -1669,8 +1677,7 @@ int flm_prg_expand(flm_ctx *ctx, const uint8_t *seeds, int K, size_t L, uint64_t
     if (int rc = hc.in(ctx->seeds.p, seeds, (size_t)K * 32)) return rc;
     if ((size_t)K * hp * 4 < kStageBytes) {  // rows written in place in the bounce buffer (flm_client_mask)
         uint8_t *bo = hc.mapped((size_t)K * hp * 4);
-        if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, reinterpret_cast<uint32_t *>(bo), hp,
-                                        ctx->stream))
+        if (int rc = flm_prg_expand_dev(ctx, ctx->seeds.as<uint8_t>(), K, L, slot0, hc.dev<uint32_t>(bo), hp, ctx->stream))
             return rc;
         hc.out_mapped(out, L * 4, bo, hp * 4, L * 4, (size_t)K);
         return hc.finish();
@@ -1739,9 +1746,9 @@ int flm_mask_accumulate(flm_ctx *ctx, const uint8_t *seeds, const int8_t *signs,
         uint8_t *bx = hc.mapped(L * 4), *by = hc.mapped(L * 4);
         ctx->copies.copy2d(bx, L * 4, acc, L * 4, L * 4, 1);
         if (int rc = upload_seeds(ctx, hc, seeds, signs, K)) return rc;
-        if (int rc = flm_aggregate_unmask_dev(ctx, reinterpret_cast<const uint32_t *>(bx), round_up(L, 4), 1,
-                                              ctx->seeds.as<uint8_t>(), ctx->signs.as<int8_t>(), K, L, 0, L, slot0,
-                                              reinterpret_cast<uint32_t *>(by), ctx->stream))
+        if (int rc = flm_aggregate_unmask_dev(ctx, hc.dev<const uint32_t>(bx), round_up(L, 4), 1, ctx->seeds.as<uint8_t>(),
+                                              ctx->signs.as<int8_t>(), K, L, 0, L, slot0, hc.dev<uint32_t>(by),
+                                              ctx->stream))
             return rc;
         hc.out_mapped(acc, L * 4, by, L * 4, L * 4, 1);
         return hc.finish();
@@ -1776,7 +1783,7 @@ int flm_chacha20_xor(flm_ctx *ctx, const uint8_t key[32], const uint8_t nonce[8]
     if (n < kStageBytes) {  // read and written in place in the bounce buffer (flm_client_mask)
         uint8_t *bi = hc.mapped(n), *bo = hc.mapped(n);
         ctx->copies.copy2d(bi, n, in, n, n, 1);
-        FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, bi, bo, n, ctx->stream));
+        FLM_HIP(ctx, flm::launch_chacha20_xor(k, nn, counter, hc.dev<const uint8_t>(bi), hc.dev<uint8_t>(bo), n, ctx->stream));
         hc.out_mapped(out, n, bo, n, n, 1);
         return hc.finish();
     }
