@@ -90,3 +90,26 @@ def test_host_pointer_calls_never_pin_caller_memory():
     assert "== done" in r.stdout
     pinned = [ln for ln in log.splitlines() if "Using Pinned resource" in ln]
     assert not pinned, "the HIP runtime pinned caller memory:\n" + "\n".join(pinned[:10])
+
+
+def test_copy_threads_end_with_their_context():
+    """A context's copy threads start on its first large host copy and are joined by flm_free: twelve
+    contexts made, used and freed leave the process with as many threads as after the first."""
+    import numpy as np
+    from flamingo_amd import MaskEngine
+
+    def nthreads():
+        return len(os.listdir("/proc/self/task"))
+
+    g = np.random.Generator(np.random.PCG64(11))
+    seeds = g.integers(0, 256, (4, 32), dtype=np.uint8)
+    after = []
+    during = None
+    for i in range(12):
+        with MaskEngine(0) as eng:
+            eng.prg_expand(seeds, 1 << 18)  # a 4 MiB output: the copy out runs on the copy threads
+            if during is None:
+                during = nthreads()
+        after.append(nthreads())
+    assert during >= after[0] + 3, (during, after)
+    assert after[-1] == after[0], after
