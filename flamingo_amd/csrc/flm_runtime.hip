@@ -1098,10 +1098,11 @@ int upload_rows(flm_ctx *ctx, const uint32_t *const *rows, int N, size_t L, uint
 // driver evicts ALL of the process's GPU queues while it revalidates: 20-40 ms in which nothing of
 // ours runs.  That was the agent run's unmask stall (the driver's per-process
 // evicted_ms grows by exactly the stall, and the stalls go away when the runtime never pins,
-// GPU_PINNED_MIN_XFER_SIZE).  The runtime's rect path (hipMemcpy2DAsync) logs no pinning but brings
-// the evictions back all the same (5 of 5 runs, profiles/r06_rect_path_evictions.log), so every
-// caller array, small or large, goes through the bounce buffer; the CPU side of the copies is split
-// over the context's CopyPool.  One bounce buffer per context: these calls are synchronous (or, for a
+// GPU_PINNED_MIN_XFER_SIZE).  The runtime's rect path (hipMemcpy2DAsync straight on the caller's
+// array) logs no pinning but brings the evictions back all the same (5 of 5 runs,
+// profiles/r06_rect_path_evictions.log), so every caller array, small or large, goes through the
+// bounce buffer; the CPU side of the copies is split over the context's CopyPool, and a call whose
+// arrays fit may run its kernel on the bounce buffer in place (mapped(), dev()).  One bounce buffer per context: these calls are synchronous (or, for a
 // group's ranks, synchronised before the call returns), so a call reuses it only after the last
 // call's copies out of it have completed; reserve() sizes it for the whole call before its first copy.
 // Copies of kStageBytes or more skip it and stream through the context's two staging buffers instead
