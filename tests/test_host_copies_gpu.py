@@ -113,3 +113,33 @@ def test_copy_threads_end_with_their_context():
         after.append(nthreads())
     assert during >= after[0] + 3, (during, after)
     assert after[-1] == after[0], after
+
+
+def test_host_calls_at_the_in_place_boundary():
+    """One-client calls run in place below 32 MiB of bounce buffer and through DMA at or above it;
+    both sides of that boundary, and tiny ragged lengths, are exact against the oracle."""
+    import numpy as np
+    sys.path.insert(0, ROOT + "/oracle")
+    import oracle as O
+    from flamingo_amd import MaskEngine
+
+    g = np.random.Generator(np.random.PCG64(13))
+    seeds = g.integers(0, 256, (3, 32), dtype=np.uint8)
+    signs = np.array([1, -1, 1], np.int8)
+    seg = np.array([0, 3], np.int64)
+    big = 8 << 20  # words: 32 MiB
+    with MaskEngine(0) as eng:
+        for L in (1, 3, 5, 1021, big - 4, big - 3, big):
+            x = g.integers(0, 2**32, (1, L), dtype=np.uint32)
+            assert np.array_equal(eng.client_mask(seg, seeds, signs, L, x=x),
+                                  O.client_mask(seg, seeds, signs, L, x=x)), L
+            acc = x[0].copy()
+            eng.mask_accumulate(seeds, signs, acc)
+            assert np.array_equal(acc, O.aggregate_unmask(x, seeds, signs, L=L)), L
+        for n in (1, 63, (32 << 20) - 1, 32 << 20):
+            data = bytes(g.integers(0, 256, n, dtype=np.uint8))
+            assert eng.chacha20_encrypt(seeds[0].tobytes(), data) == O.chacha20_encrypt(seeds[0].tobytes(), data), n
+        for K, L in ((2, (4 << 20) - 4), (2, 4 << 20), (1, 7)):  # K x L words: just under, at 32 MiB; tiny
+            e = eng.prg_expand(seeds[:K], L)
+            for k in range(K):
+                assert np.array_equal(e[k], O.prg(seeds[k].tobytes(), L, 0)), (K, L, k)
